@@ -1,0 +1,150 @@
+/*
+ * qg_mi355.h -- C-ABI of the MI355X-native two-layer Phillips (baroclinic QG) hot path.
+ *
+ * Drop-in boundary for the reference's per-timestep path
+ * (JSLeadbetter/julia-ocean-modelling @ 2024-10-08, paths relative to its root):
+ *
+ *   evolve_zeta!(model, zeta, psi, timestep, f_store)      src/model.jl:155-170
+ *   evolve_psi!(model, zeta, psi, poisson_chol, helm_chol) src/model.jl:172-199
+ *   get_poisson_cholesky / get_helmholtz_cholesky          src/schemes/laplacian.jl:60-75
+ *   run_model_no_output(model)                             src/run_model_no_output.jl:3-16
+ *   initialise_model(model)                                src/model.jl:37-62
+ *   J, laplace_5p, cd, update_doubly_periodic_bc!          arakawa.jl:58, laplacian.jl:15,
+ *                                                          model.jl:68, boundary_conditions.jl:2
+ *   sp_solve_modified_helmholtz / sp_solve_poisson         src/schemes/laplacian.jl:78-111
+ *
+ * Conventions (identical to the reference's arrays):
+ *   - every field is IEEE Float64, Julia column-major (M+2) x (P+2) with a one-cell ghost
+ *     ring: element (i, j) (0-based, ghosts included) lives at  ptr[i + (M+2)*j];
+ *   - the model state zeta, psi, f_store are (M+2, P+2, 2, 3) arrays: layer l (0/1) and
+ *     history slot s (0/1/2) of field X start at X + (M+2)*(P+2)*(l + 2*s);
+ *   - all pointers are DEVICE pointers owned by the caller (the library never frees them);
+ *   - all work is enqueued on the stream given at creation (a hipStream_t passed as void*);
+ *     entry points return once the work is enqueued unless documented otherwise;
+ *   - every entry point returns 0 on success or a negative qg_status; qg_strerror() names it.
+ *     A call that fails leaves the state untouched where it can, and never falls back to a
+ *     CPU path.
+ *
+ * History slots.  The reference shifts slots 3<-2<-1 on every store_new_state! (copies of
+ * whole fields).  The library keeps the same three physical slots but rotates a head index
+ * instead of copying: after a step the newest field is in slot qg_slot(ctx, which, 1), the
+ * previous one in qg_slot(ctx, which, 2), the one before in qg_slot(ctx, which, 3) -- exactly
+ * the reference's contents, permuted.  qg_canonicalize() physically restores the reference
+ * order (slot 1 first) when a caller needs the arrays back in that order.
+ *
+ * Multi-GPU: the y-direction (second index) is split into slabs, one rank per GPU; every
+ * rank passes its LOCAL P and binds local (M+2, P_local+2, 2, 3) arrays.  Halo rows move
+ * with RCCL send/recv; the streamfunction inversion needs one small all-gather per step.
+ */
+#ifndef QG_MI355_H
+#define QG_MI355_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QG_ABI_VERSION 1
+
+typedef enum {
+    QG_OK = 0,
+    QG_ERR_INVALID_ARG = -1,  /* bad pointer / size / parameter                         */
+    QG_ERR_UNSUPPORTED = -2,  /* configuration the selected solver cannot handle         */
+    QG_ERR_HIP = -3,          /* a HIP runtime call failed (launch, alloc, copy)         */
+    QG_ERR_NOT_BOUND = -4,    /* state arrays not bound / not initialised               */
+    QG_ERR_ALLOC = -5,        /* device allocation failed                                */
+    QG_ERR_RCCL = -6,         /* an RCCL call failed or no communicator was set up       */
+    QG_ERR_NOT_CONVERGED = -7 /* PCG reached pcg_maxit above pcg_rtol (result is kept)   */
+} qg_status;
+
+typedef enum {
+    QG_SOLVER_SPECTRAL = 0, /* direct: x-DFT + parallel cyclic tridiagonal solve in y     */
+    QG_SOLVER_PCG = 1       /* matrix-free PCG on the 5-point operator                     */
+} qg_solver_kind;
+
+typedef enum {
+    QG_PRECOND_NONE = 0,    /* plain CG                                                    */
+    QG_PRECOND_SPECTRAL = 1 /* the spectral direct solve as preconditioner                 */
+} qg_precond_kind;
+
+/* BaroclinicModel (src/model.jl:12-30) plus build options.  Fill with qg_default_params()
+ * first, then set the model fields.  M, P are the interior node counts (P per rank). */
+typedef struct qg_params {
+    double H_1, H_2, beta, Lx, Ly, dt, T, U;
+    int64_t M, P;
+    double dx, visc, r, R_d, initial_kick;
+    /* back-projection psi_l = P_fwd[2l]*psi~_1 + P_fwd[2l+1]*psi~_2.  Default: the
+     * reference's P_matrix(H_1, H_1) = [[1,-1],[1,1]] (src/model.jl:173).           */
+    double P_fwd[4];
+    int32_t solver;     /* qg_solver_kind (default QG_SOLVER_SPECTRAL)                  */
+    int32_t precond;    /* qg_precond_kind for QG_SOLVER_PCG (default SPECTRAL)         */
+    double pcg_rtol;    /* relative residual target ||b-Ax||/||b|| (default 1e-13)      */
+    int32_t pcg_maxit;  /* default 500                                                  */
+    int32_t chunk_rows; /* y-chunk of the spectral solver; 0 = automatic                */
+} qg_params;
+
+typedef struct qg_ctx qg_ctx;       /* one model instance (one rank) on one device       */
+typedef struct qg_solver qg_solver; /* a pair of 5-point periodic solves (the "factors") */
+
+/* per-step solver statistics (host-side copy; reading them synchronises the stream) */
+typedef struct qg_stats {
+    int32_t iters[2];    /* PCG iterations of the Poisson / Helmholtz solve (0 = direct) */
+    double relres[2];    /* ||b - A x|| / ||b|| of the last solve (if measured, else -1) */
+    double delta;        /* Poisson compatibility adjustment applied at interior (1,1)   */
+    double pin;          /* value subtracted from the Poisson solution (pinning)         */
+} qg_stats;
+
+int qg_abi_version(void);
+const char *qg_strerror(int status);
+void qg_default_params(qg_params *p);
+
+/* ---- model context (replaces the state arrays + the two CHOLMOD factors) ------------ */
+int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out);
+int qg_destroy(qg_ctx *ctx);
+/* zeta, psi, f_store: device (M+2, P+2, 2, 3) Float64 arrays owned by the caller */
+int qg_bind_state(qg_ctx *ctx, double *zeta, double *psi, double *f_store);
+/* initialise_model (model.jl:37-62) on the device, seeded: psi_l interior (i, j) =
+ * kick*U*Ly*u01(seed_l, i + M*j_global); zeroes all other slots and f_store; resets the
+ * slot rotation. */
+int qg_initialise(qg_ctx *ctx, uint64_t seed1, uint64_t seed2);
+int qg_evolve_zeta(qg_ctx *ctx, int64_t timestep); /* 1-based; Euler for 1, 2, AB3 after */
+int qg_evolve_psi(qg_ctx *ctx);
+int qg_step(qg_ctx *ctx, int64_t timestep);        /* evolve_zeta! then evolve_psi!       */
+int qg_run(qg_ctx *ctx, int64_t first_step, int64_t nsteps);
+/* which: 0 = zeta, 1 = psi, 2 = f_store; logical 1..3 -> physical 0..2 */
+int qg_slot(const qg_ctx *ctx, int which, int logical, int *physical);
+int qg_set_slots(qg_ctx *ctx, const int heads[3]); /* restore a saved rotation (resume)  */
+int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2,3       */
+int qg_get_stats(qg_ctx *ctx, qg_stats *out);
+int qg_synchronize(qg_ctx *ctx);
+
+/* ---- multi-GPU (one rank per GPU, slab decomposition in y) --------------------------- */
+int qg_comm_unique_id(char out[128]);               /* ncclGetUniqueId on rank 0          */
+int qg_comm_init(qg_ctx *ctx, int nranks, int rank, const char id[128]);
+
+/* ---- solver handle: the get_*_cholesky analogue --------------------------------------
+ * Solves, for s = 0, 1,   A_s x_s = g_s  with A_s = construct_spA(M, P, dx, alpha[s])
+ * (the periodic 5-point operator + alpha I, src/schemes/laplacian.jl:54-58) and
+ *   g_s = proj_in[2s]*f_1 + proj_in[2s+1]*f_2          (interior of the input fields),
+ * pinned[s] != 0 selects the pinned Poisson system of get_poisson_cholesky (alpha must be 0;
+ * solution is 0 at interior (1,1)), then writes
+ *   out_l = proj_out[2l]*x_1 + proj_out[2l+1]*x_2       with the periodic ghost ring.
+ * f_2 / out_2 may be NULL when proj_in / proj_out do not need them.                        */
+int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], const int pinned[2],
+                     const double proj_in[4], const double proj_out[4], int kind, int precond,
+                     int device, void *stream, qg_solver **out);
+int qg_solver_solve(qg_solver *s, const double *f_1, const double *f_2, double *out_1, double *out_2);
+int qg_solver_destroy(qg_solver *s);
+
+/* ---- stateless kernels on (M+2, P+2) device fields (ghost ring refreshed on output) ---- */
+int qg_laplace_5p(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream);
+int qg_cd(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream);
+int qg_arakawa_J(const double *zeta, const double *psi, double *out, int64_t M, int64_t P,
+                 double dx, void *stream);
+int qg_fill_ghosts(double *b, int64_t M, int64_t P, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QG_MI355_H */

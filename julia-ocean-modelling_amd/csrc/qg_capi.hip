@@ -1,0 +1,392 @@
+// C-ABI implementation (include/qg_mi355.h): model context, slot rotation, solver handles,
+// stateless operators.  Everything is enqueued on the caller's stream; nothing in a step
+// allocates, synchronises or touches the host.
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <new>
+
+#include "qg_common.hpp"
+#include "qg_spectral.hpp"
+
+namespace qg {
+int comm_destroy(void *comm);
+int comm_allgather(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
+int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
+              hipStream_t s);
+int comm_init(void **comm, int nranks, int rank, const char id[128]);
+int comm_unique_id(char out[128]);
+}  // namespace qg
+
+using namespace qg;
+
+struct qg_solver {
+    SpectralSolver spec;
+    hipStream_t stream = nullptr;
+    int device = 0;
+};
+
+struct qg_ctx {
+    qg_params p{};
+    Derived d{};
+    int device = 0;
+    hipStream_t stream = nullptr;
+    double *zeta = nullptr, *psi = nullptr, *fst = nullptr;
+    int heads[3] = {0, 0, 0};  // physical slot of logical slot 1 for zeta, psi, f_store
+    bool initialised = false;
+    int rank = 0, nranks = 1;
+    void *comm = nullptr;        // RCCL communicator wrapper (multi-GPU)
+    double *halo = nullptr;      // received halo rows (multi-GPU)
+    std::unique_ptr<SpectralSolver> spec;
+    size_t F = 0;  // doubles per (M+2, P+2) field
+
+    double *field(double *base, int layer, int slot) const { return base + F * (size_t)(layer + 2 * slot); }
+};
+
+extern "C" {
+
+int qg_abi_version(void) { return QG_ABI_VERSION; }
+
+const char *qg_strerror(int s) {
+    switch (s) {
+        case QG_OK: return "ok";
+        case QG_ERR_INVALID_ARG: return "invalid argument";
+        case QG_ERR_UNSUPPORTED: return "unsupported configuration";
+        case QG_ERR_HIP: return "HIP runtime error";
+        case QG_ERR_NOT_BOUND: return "state not bound / not initialised";
+        case QG_ERR_ALLOC: return "device allocation failed";
+        case QG_ERR_RCCL: return "RCCL error or no communicator";
+        case QG_ERR_NOT_CONVERGED: return "PCG did not converge";
+        default: return "unknown status";
+    }
+}
+
+void qg_default_params(qg_params *p) {
+    if (!p) return;
+    std::memset(p, 0, sizeof(*p));
+    p->P_fwd[0] = 1.0;  // P_matrix(H_1, H_1): [[1, -H_1/H_1], [1, 1]]  (model.jl:173)
+    p->P_fwd[1] = -1.0;
+    p->P_fwd[2] = 1.0;
+    p->P_fwd[3] = 1.0;
+    p->solver = QG_SOLVER_SPECTRAL;
+    p->precond = QG_PRECOND_SPECTRAL;
+    p->pcg_rtol = 1e-13;
+    p->pcg_maxit = 500;
+    p->chunk_rows = 0;
+}
+
+static int check_params(const qg_params *p) {
+    if (!p) return QG_ERR_INVALID_ARG;
+    if (p->M < 2 || p->P < 2 || !(p->dx > 0) || !(p->H_1 > 0) || !(p->H_2 > 0) || !(p->R_d > 0))
+        return QG_ERR_INVALID_ARG;
+    if (p->solver != QG_SOLVER_SPECTRAL && p->solver != QG_SOLVER_PCG) return QG_ERR_INVALID_ARG;
+    return QG_OK;
+}
+
+static int build_solver(qg_ctx *c) {
+    const qg_params &p = c->p;
+    if (p.solver != QG_SOLVER_SPECTRAL) return QG_ERR_UNSUPPORTED;
+    if (!SpectralSolver::supports(p.M, p.P)) return QG_ERR_UNSUPPORTED;
+    auto s = std::make_unique<SpectralSolver>();
+    const double alpha[2] = {0.0, c->d.Seig};
+    QG_HIP(hipSetDevice(c->device));
+    QG_CHECK(s->init(p.M, p.P, p.P * c->nranks, c->rank, c->nranks, p.dx, alpha, 1, c->d.Pinv, p.P_fwd,
+                     p.chunk_rows));
+    c->spec = std::move(s);
+    return QG_OK;
+}
+
+int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out) {
+    if (!out) return QG_ERR_INVALID_ARG;
+    *out = nullptr;
+    QG_CHECK(check_params(p));
+    qg_ctx *c = new (std::nothrow) qg_ctx();
+    if (!c) return QG_ERR_ALLOC;
+    c->p = *p;
+    c->d = derive(*p);
+    c->device = device;
+    c->stream = static_cast<hipStream_t>(stream);
+    c->F = (size_t)(p->M + 2) * (size_t)(p->P + 2);
+    // beta_1 and beta_2 must have opposite signs (model.jl:38)
+    if (!((c->d.beta1 > 0 && c->d.beta2 < 0) || (c->d.beta1 < 0 && c->d.beta2 > 0))) {
+        delete c;
+        return QG_ERR_INVALID_ARG;
+    }
+    int st = build_solver(c);
+    if (st != QG_OK) {
+        delete c;
+        return st;
+    }
+    *out = c;
+    return QG_OK;
+}
+
+int qg_destroy(qg_ctx *c) {
+    if (!c) return QG_OK;
+    (void)hipSetDevice(c->device);
+    if (c->comm) comm_destroy(c->comm);
+    if (c->halo) (void)hipFree(c->halo);
+    delete c;
+    return QG_OK;
+}
+
+int qg_bind_state(qg_ctx *c, double *zeta, double *psi, double *f_store) {
+    if (!c || !zeta || !psi || !f_store) return QG_ERR_INVALID_ARG;
+    c->zeta = zeta;
+    c->psi = psi;
+    c->fst = f_store;
+    c->heads[0] = c->heads[1] = c->heads[2] = 0;
+    c->initialised = true;  // caller-provided contents are taken as the reference layout
+    return QG_OK;
+}
+
+int qg_initialise(qg_ctx *c, uint64_t seed1, uint64_t seed2) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    if (!c->zeta) return QG_ERR_NOT_BOUND;
+    const qg_params &p = c->p;
+    QG_HIP(hipSetDevice(c->device));
+    const double amp = p.initial_kick * p.U * p.Ly;
+    QG_CHECK(launch_initialise_global(c->zeta, c->psi, c->fst, p.M, p.P, p.P * c->nranks,
+                                      (int64_t)c->rank * p.P, amp, c->d.S1, c->d.S2, p.dx, seed1, seed2,
+                                      c->stream));
+    c->heads[0] = c->heads[1] = c->heads[2] = 0;
+    c->initialised = true;
+    return QG_OK;
+}
+
+int qg_slot(const qg_ctx *c, int which, int logical, int *physical) {
+    if (!c || !physical || which < 0 || which > 2 || logical < 1 || logical > 3) return QG_ERR_INVALID_ARG;
+    *physical = (c->heads[which] + logical - 1) % 3;
+    return QG_OK;
+}
+
+int qg_set_slots(qg_ctx *c, const int heads[3]) {
+    if (!c || !heads) return QG_ERR_INVALID_ARG;
+    for (int k = 0; k < 3; ++k)
+        if (heads[k] < 0 || heads[k] > 2) return QG_ERR_INVALID_ARG;
+    for (int k = 0; k < 3; ++k) c->heads[k] = heads[k];
+    return QG_OK;
+}
+
+static void fill_wrap_rows(const qg_ctx *c, const double *base, RowSrc &rs) {
+    // single-GPU: rows -2,-1,P,P+1 are the periodic images P-2,P-1,0,1
+    const int64_t P = c->p.P, ld = c->p.M + 2;
+    const int64_t rows[4] = {(P - 2 + P) % P, P - 1, 0, 1 % P};
+    for (int h = 0; h < 4; ++h) rs.halo[h] = base + fidx(1, rows[h] + 1, ld);
+}
+
+int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
+    if (!c || timestep < 1) return QG_ERR_INVALID_ARG;
+    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
+    if (c->nranks > 1 && !c->comm) return QG_ERR_RCCL;
+    const qg_params &p = c->p;
+    QG_HIP(hipSetDevice(c->device));
+    const int zh = c->heads[0], ph = c->heads[1], fh = c->heads[2];
+    const int zn = (zh + 2) % 3, fn = (fh + 2) % 3;
+    TendArgs a{};
+    a.M = p.M;
+    a.P = p.P;
+    a.ld = p.M + 2;
+    a.dx = p.dx;
+    a.visc = p.visc;
+    a.dt = p.dt;
+    a.U = p.U;
+    a.r = p.r;
+    a.beta[0] = c->d.beta1;
+    a.beta[1] = c->d.beta2;
+    a.ab3 = timestep >= 3;
+    a.j0 = 0;
+    a.j1 = (int)p.P;
+    a.write_ghost_rows = c->nranks == 1;
+    for (int l = 0; l < 2; ++l) {
+        a.zeta[l] = c->field(c->zeta, l, zh);
+        a.psi[l] = c->field(c->psi, l, ph);
+        a.fprev1[l] = c->field(c->fst, l, fh);
+        a.fprev2[l] = c->field(c->fst, l, (fh + 1) % 3);
+        a.zeta_out[l] = c->field(c->zeta, l, zn);
+        a.f_out[l] = c->field(c->fst, l, fn);
+    }
+    if (c->nranks == 1) {
+        for (int l = 0; l < 2; ++l) {
+            fill_wrap_rows(c, a.zeta[l], a.zeta_rows[l]);
+            fill_wrap_rows(c, a.psi[l], a.psi_rows[l]);
+        }
+    } else {
+        // halo rows of psi (depth 2) and zeta (depth 1) from the neighbouring slabs
+        double *fields[4] = {const_cast<double *>(a.psi[0]), const_cast<double *>(a.psi[1]),
+                             const_cast<double *>(a.zeta[0]), const_cast<double *>(a.zeta[1])};
+        QG_CHECK(comm_halo(c->comm, fields, 4, p.M, p.P, 2, c->halo, c->stream));
+        const int64_t row = p.M + 2;  // halo buffer: [field][4 rows][M+2]; +1 = interior start
+        for (int l = 0; l < 2; ++l)
+            for (int h = 0; h < 4; ++h) {
+                a.psi_rows[l].halo[h] = c->halo + ((size_t)(l * 4 + h)) * row + 1;
+                a.zeta_rows[l].halo[h] = c->halo + ((size_t)((2 + l) * 4 + h)) * row + 1;
+            }
+    }
+    QG_CHECK(launch_tendency(a, c->stream));
+    if (c->nranks > 1) {  // ghost rows of the new zeta and F from the neighbours
+        double *fields[4] = {a.zeta_out[0], a.zeta_out[1], a.f_out[0], a.f_out[1]};
+        QG_CHECK(comm_halo(c->comm, fields, 4, p.M, p.P, -1, nullptr, c->stream));
+    }
+    c->heads[0] = zn;
+    c->heads[2] = fn;
+    return QG_OK;
+}
+
+int qg_evolve_psi(qg_ctx *c) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
+    if (!c->spec) return QG_ERR_UNSUPPORTED;
+    if (c->nranks > 1 && !c->comm) return QG_ERR_RCCL;
+    QG_HIP(hipSetDevice(c->device));
+    const int zh = c->heads[0], pn = (c->heads[1] + 2) % 3;
+    double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);
+    QG_CHECK(c->spec->solve(c->field(c->zeta, 0, zh), c->field(c->zeta, 1, zh), o1, o2, c->nranks == 1, c->stream,
+                            c->nranks > 1 ? comm_allgather : nullptr, c->comm));
+    if (c->nranks > 1) {  // ghost rows of the new psi from the neighbours (drop-in ghost ring)
+        double *fields[2] = {o1, o2};
+        QG_CHECK(comm_halo(c->comm, fields, 2, c->p.M, c->p.P, -1, nullptr, c->stream));
+    }
+    c->heads[1] = pn;
+    return QG_OK;
+}
+
+int qg_step(qg_ctx *c, int64_t timestep) {
+    QG_CHECK(qg_evolve_zeta(c, timestep));
+    return qg_evolve_psi(c);
+}
+
+int qg_run(qg_ctx *c, int64_t first_step, int64_t nsteps) {
+    if (!c || first_step < 1 || nsteps < 0) return QG_ERR_INVALID_ARG;
+    for (int64_t t = first_step; t < first_step + nsteps; ++t) QG_CHECK(qg_step(c, t));
+    return QG_OK;
+}
+
+int qg_canonicalize(qg_ctx *c) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    if (!c->zeta) return QG_ERR_NOT_BOUND;
+    QG_HIP(hipSetDevice(c->device));
+    double *bases[3] = {c->zeta, c->psi, c->fst};
+    double *tmp = nullptr;
+    const size_t bytes = sizeof(double) * c->F * 6;
+    for (int w = 0; w < 3; ++w) {
+        if (c->heads[w] == 0) continue;
+        if (!tmp) QG_HIP(hipMallocAsync((void **)&tmp, bytes, c->stream));
+        QG_HIP(hipMemcpyAsync(tmp, bases[w], bytes, hipMemcpyDeviceToDevice, c->stream));
+        for (int logical = 1; logical <= 3; ++logical) {
+            const int phys = (c->heads[w] + logical - 1) % 3;
+            for (int l = 0; l < 2; ++l)
+                QG_HIP(hipMemcpyAsync(c->field(bases[w], l, logical - 1), tmp + c->F * (size_t)(l + 2 * phys),
+                                      sizeof(double) * c->F, hipMemcpyDeviceToDevice, c->stream));
+        }
+        c->heads[w] = 0;
+    }
+    if (tmp) QG_HIP(hipFreeAsync(tmp, c->stream));
+    return QG_OK;
+}
+
+int qg_get_stats(qg_ctx *c, qg_stats *out) {
+    if (!c || !out) return QG_ERR_INVALID_ARG;
+    std::memset(out, 0, sizeof(*out));
+    out->relres[0] = out->relres[1] = -1;
+    if (!c->spec) return QG_OK;
+    double sc[2];
+    QG_HIP(hipSetDevice(c->device));
+    QG_HIP(hipMemcpyAsync(sc, c->spec->args().scal, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
+    QG_HIP(hipStreamSynchronize(c->stream));
+    out->delta = sc[0];
+    out->pin = sc[1];
+    return QG_OK;
+}
+
+int qg_synchronize(qg_ctx *c) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    QG_HIP(hipSetDevice(c->device));
+    QG_HIP(hipStreamSynchronize(c->stream));
+    return QG_OK;
+}
+
+// ---- multi-GPU -------------------------------------------------------------------------
+int qg_comm_unique_id(char out[128]) {
+    if (!out) return QG_ERR_INVALID_ARG;
+    return comm_unique_id(out);
+}
+
+int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return QG_ERR_INVALID_ARG;
+    QG_HIP(hipSetDevice(c->device));
+    if (c->comm) {
+        comm_destroy(c->comm);
+        c->comm = nullptr;
+    }
+    QG_CHECK(comm_init(&c->comm, nranks, rank, id));
+    c->rank = rank;
+    c->nranks = nranks;
+    if (!c->halo) QG_HIP(hipMalloc((void **)&c->halo, sizeof(double) * 16 * (size_t)(c->p.M + 2)));
+    return build_solver(c);
+}
+
+// ---- solver handles ---------------------------------------------------------------------
+int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], const int pinned[2],
+                     const double proj_in[4], const double proj_out[4], int kind, int precond, int device,
+                     void *stream, qg_solver **out) {
+    (void)precond;
+    if (!out || !alpha || !pinned || !proj_in || !proj_out) return QG_ERR_INVALID_ARG;
+    *out = nullptr;
+    if (kind != QG_SOLVER_SPECTRAL) return QG_ERR_UNSUPPORTED;
+    if (pinned[1]) return QG_ERR_UNSUPPORTED;           // only system 0 may be the pinned Poisson
+    if (pinned[0] && alpha[0] != 0.0) return QG_ERR_INVALID_ARG;
+    qg_solver *s = new (std::nothrow) qg_solver();
+    if (!s) return QG_ERR_ALLOC;
+    s->device = device;
+    s->stream = static_cast<hipStream_t>(stream);
+    if (hipSetDevice(device) != hipSuccess) {
+        delete s;
+        return QG_ERR_HIP;
+    }
+    const int st = s->spec.init(M, P, P, 0, 1, dx, alpha, pinned[0], proj_in, proj_out, 0);
+    if (st != QG_OK) {
+        delete s;
+        return st;
+    }
+    *out = s;
+    return QG_OK;
+}
+
+int qg_solver_solve(qg_solver *s, const double *f_1, const double *f_2, double *out_1, double *out_2) {
+    if (!s || !f_1 || !out_1) return QG_ERR_INVALID_ARG;
+    QG_HIP(hipSetDevice(s->device));
+    return s->spec.solve(f_1, f_2, out_1, out_2, 1, s->stream);
+}
+
+int qg_solver_destroy(qg_solver *s) {
+    if (s) {
+        (void)hipSetDevice(s->device);
+        delete s;
+    }
+    return QG_OK;
+}
+
+// ---- stateless operators ----------------------------------------------------------------
+int qg_laplace_5p(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream) {
+    if (!u || !out || M < 1 || P < 1 || !(dx > 0)) return QG_ERR_INVALID_ARG;
+    return launch_laplace(u, out, M, P, dx, static_cast<hipStream_t>(stream));
+}
+
+int qg_cd(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream) {
+    if (!u || !out || M < 1 || P < 1 || !(dx > 0)) return QG_ERR_INVALID_ARG;
+    return launch_cd(u, out, M, P, dx, static_cast<hipStream_t>(stream));
+}
+
+int qg_arakawa_J(const double *zeta, const double *psi, double *out, int64_t M, int64_t P, double dx,
+                 void *stream) {
+    if (!zeta || !psi || !out || M < 1 || P < 1 || !(dx > 0)) return QG_ERR_INVALID_ARG;
+    return launch_arakawa(zeta, psi, out, M, P, dx, static_cast<hipStream_t>(stream));
+}
+
+int qg_fill_ghosts(double *b, int64_t M, int64_t P, void *stream) {
+    if (!b || M < 1 || P < 1) return QG_ERR_INVALID_ARG;
+    return launch_fill_ghosts(b, M, P, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,134 @@
+// Shared helpers for the gfx950 QG kernels and the C-ABI implementation.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "qg_mi355.h"
+
+#define QG_HIP(call)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            std::fprintf(stderr, "qg_mi355: %s failed: %s (%s:%d)\n", #call,           \
+                         hipGetErrorString(e_), __FILE__, __LINE__);                   \
+            return QG_ERR_HIP;                                                         \
+        }                                                                              \
+    } while (0)
+
+#define QG_CHECK(expr)                                                                 \
+    do {                                                                               \
+        int s_ = (expr);                                                               \
+        if (s_ != QG_OK) return s_;                                                    \
+    } while (0)
+
+#define QG_LAUNCH_CHECK() QG_HIP(hipGetLastError())
+
+namespace qg {
+
+constexpr int WAVE = 64;
+
+__host__ __device__ inline size_t fidx(int64_t i, int64_t j, int64_t ld) {
+    return static_cast<size_t>(i) + static_cast<size_t>(ld) * static_cast<size_t>(j);
+}
+
+// complex helpers on double2 (x = re, y = im)
+__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+    return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
+__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+
+// Write v at interior (i, j) and at every ghost cell that is a periodic image of it
+// (edges and the diagonal corners of update_doubly_periodic_bc!).  ghost_rows = 0 skips the
+// images in rows -1 / P (multi-GPU slabs get those rows from their neighbours).
+__device__ __forceinline__ void store_with_ghosts(double *out, int64_t ld, int64_t M, int64_t P,
+                                                  int64_t i, int64_t j, double v, bool ghost_rows) {
+    const int64_t mi = i + 1, mj = j + 1;
+    out[fidx(mi, mj, ld)] = v;
+    const bool lo_i = (i == 0), hi_i = (i == M - 1);
+    if (hi_i) out[fidx(0, mj, ld)] = v;
+    if (lo_i) out[fidx(M + 1, mj, ld)] = v;
+    if (ghost_rows) {
+        const bool lo_j = (j == 0), hi_j = (j == P - 1);
+        if (hi_j) out[fidx(mi, 0, ld)] = v;
+        if (lo_j) out[fidx(mi, P + 1, ld)] = v;
+        if (hi_i && hi_j) out[fidx(0, 0, ld)] = v;
+        if (hi_i && lo_j) out[fidx(0, P + 1, ld)] = v;
+        if (lo_i && lo_j) out[fidx(M + 1, P + 1, ld)] = v;
+        if (lo_i && hi_j) out[fidx(M + 1, 0, ld)] = v;
+    }
+}
+
+// counter-based uniform in [0,1) shared with oracle/qg_ref.py and oracle/qg_oracle.c
+__host__ __device__ inline double u01(uint64_t seed, uint64_t k) {
+    uint64_t x = seed + (k + 1) * 0x9E3779B97F4A7C15ULL;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+    x = x ^ (x >> 31);
+    return static_cast<double>(x >> 11) * 0x1.0p-53;
+}
+
+// Model-derived constants, in the reference's evaluation order (src/model.jl:109-121).
+struct Derived {
+    double ratio, S1, S2, beta1, beta2, Seig;
+    double Pinv[4];  // P_inv_matrix (model.jl:90-99), row-major
+};
+
+inline Derived derive(const qg_params &m) {
+    Derived d;
+    d.ratio = 0.5 * (m.H_1 + m.H_2) / ((m.R_d * m.R_d) * ((1 / m.H_1) + (1 / m.H_2)));
+    d.S1 = (2 * d.ratio) / (m.H_1 * (m.H_1 + m.H_2));
+    d.S2 = (2 * d.ratio) / (m.H_2 * (m.H_1 + m.H_2));
+    d.beta1 = m.beta + (d.S1 * m.U);
+    d.beta2 = m.beta - (d.S2 * m.U);
+    d.Seig = -1 / (m.R_d * m.R_d);
+    const double a = d.S1, b = d.S2, c = 1 / (a + b);
+    d.Pinv[0] = c * b;
+    d.Pinv[1] = c * a;
+    d.Pinv[2] = c * -b;
+    d.Pinv[3] = c * b;
+    return d;
+}
+
+// ---- stencil / tendency launchers (qg_stencil.hip) ----------------------------------
+struct RowSrc {
+    // Rows outside [0, P) of a field come from these pointers (interior element 0 of the
+    // row, i.e. already offset by the left ghost): index 0,1 = rows -2,-1; 2,3 = rows P, P+1.
+    const double *halo[4];
+};
+
+struct TendArgs {
+    int64_t M, P, ld;          // interior sizes; ld = M + 2
+    double dx, visc, dt, U, r;
+    double beta[2];
+    int ab3;                   // 0 = Euler, 1 = AB3
+    int j0, j1;                // output row range [j0, j1)
+    int write_ghost_rows;      // single-GPU: refresh ghost rows -1 and P
+    // per layer pointers (field base = element (0,0) incl. ghosts)
+    const double *zeta[2];
+    const double *psi[2];
+    const double *fprev1[2];   // F(t-1), F(t-2) for AB3
+    const double *fprev2[2];
+    double *zeta_out[2];
+    double *f_out[2];
+    RowSrc zeta_rows[2];
+    RowSrc psi_rows[2];
+};
+
+int launch_tendency(const TendArgs &a, hipStream_t s);
+int launch_laplace(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
+int launch_cd(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
+int launch_arakawa(const double *z, const double *p, double *out, int64_t M, int64_t P, double dx,
+                   hipStream_t s);
+int launch_fill_ghosts(double *b, int64_t M, int64_t P, hipStream_t s);
+int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s);
+int launch_initialise_global(double *zeta, double *psi, double *f_store, int64_t M, int64_t P,
+                             int64_t P_total, int64_t j_offset, double amp, double S1, double S2,
+                             double dx, uint64_t seed1, uint64_t seed2, hipStream_t s);
+
+}  // namespace qg

@@ -1,0 +1,576 @@
+// Spectral (FACR) direct solver kernels for gfx950 -- see qg_spectral.hpp for the method.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "qg_fft.hpp"
+#include "qg_spectral.hpp"
+
+namespace qg {
+
+constexpr int CARRY_WAVES = 8;
+constexpr int PIN_THREADS = 1024;
+
+template <int N>
+struct Geo {
+    static constexpr int T = N / 8 < 64 ? 64 : (N / 8 > 512 ? 512 : N / 8);  // threads per row
+    static constexpr int KH = N / 2 + 1;
+    static constexpr int KQ = (KH + T - 1) / T;  // wavenumbers per thread
+    static constexpr int EP = (N + T - 1) / T;   // row elements per thread
+};
+
+__device__ __forceinline__ double2 cfma(double s, double2 x, double2 y) {  // s*x + y
+    return make_double2(s * x.x + y.x, s * x.y + y.y);
+}
+
+// ------------------------------------------------------------------------------------
+// pass A: project + row DFT + chunk-local backward filter (one workgroup per chunk)
+// ------------------------------------------------------------------------------------
+template <int N>
+__global__ __launch_bounds__(Geo<N>::T) void spec_passA(SpecArgs a) {
+    using G = Geo<N>;
+    constexpr int T = G::T, KH = G::KH, KQ = G::KQ, EP = G::EP;
+    extern __shared__ double2 buf[];
+    const int t = threadIdx.x, c = blockIdx.x;
+    const int s0 = c * a.L, e = s0 + a.L - 1;
+    const int KS = a.KS;
+    const int64_t ld = a.ld;
+    double2 u[KQ][2], wl[KQ][2];
+    double wg[KQ][2];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            u[q][s] = make_double2(0, 0);
+            wl[q][s] = make_double2(0, 0);
+            wg[q][s] = 1.0;
+        }
+    double dc = 0;
+    double *hline = a.rec + rec_HLINE(KS);
+    for (int j = e; j >= s0; --j) {
+        const double *r1 = a.in1 + fidx(1, j + 1, ld);
+        const double *r2 = a.in2 + fidx(1, j + 1, ld);
+#pragma unroll
+        for (int p = 0; p < EP; ++p) {
+            const int i = t + p * T;
+            if (N % T == 0 || i < N) {
+                const double x1 = r1[i], x2 = r2[i];
+                buf[i] = make_double2(a.pin_in[0] * x1 + a.pin_in[1] * x2, a.pin_in[2] * x1 + a.pin_in[3] * x2);
+            }
+        }
+        __syncthreads();
+        fft_lds<N, T, false>(buf, a.tw);
+        double2 *Urow = a.U + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+            const int k = t + q * T;
+            if (KH % T == 0 || k < KH) {
+                const double2 Zk = buf[k], Zm = buf[(N - k) & (N - 1)];
+                double2 B[2];
+                B[0] = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
+                B[1] = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
+                if (k == 0) {
+                    dc += B[0].x;
+                    hline[j] = B[0].x;
+                }
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const double r = a.coef[s * KS + k].r;
+                    u[q][s] = cfma(r, u[q][s], B[s]);
+                    Urow[s * KS + k] = u[q][s];
+                    wl[q][s] = cfma(wg[q][s], u[q][s], wl[q][s]);
+                    wg[q][s] *= r;
+                }
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+        const int k = t + q * T;
+        if (KH % T == 0 || k < KH) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                a.ULS[((size_t)c * 2 + s) * KS + k] = u[q][s];
+                a.WLS[((size_t)c * 2 + s) * KS + k] = wl[q][s];
+            }
+        }
+    }
+    if (t == 0) a.dcpart[c] = dc;
+}
+
+// ------------------------------------------------------------------------------------
+// carry: segment-parallel chunk scans.  Lanes = 64 consecutive k of one system, waves =
+// contiguous segments of chunks.  Zero carries at the rank boundaries (cross-rank and
+// periodic closure are applied by spec_pin / spec_passB).
+//   v_c = ULS_c + q v_{c+1}, v_Nc = 0      UIN_c = v_{c+1},  AU = v_0
+//   w_c = (WLS_c + gam UIN_c) + q w_{c-1}   WIN_c = w_{c-1},  AW = w_{Nc-1}
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
+    __shared__ double2 agg[CARRY_WAVES][64];
+    __shared__ double qlen_s[CARRY_WAVES][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int W = CARRY_WAVES;
+    const int k = blockIdx.x * 64 + lane, s = blockIdx.y;
+    const bool ok = k < a.KH;
+    const int KS = a.KS, Nc = a.Nc;
+    const int SL = (Nc + W - 1) / W;
+    const int c0 = min(wv * SL, Nc), c1 = min(c0 + SL, Nc);
+    double q = 0, gam = 0;
+    if (ok) {
+        q = a.coef[s * KS + k].q;
+        gam = a.coef[s * KS + k].gam;
+    }
+    auto at = [&](const double2 *base, int c) { return base[((size_t)c * 2 + s) * KS + k]; };
+    auto put = [&](double2 *base, int c, double2 v) { base[((size_t)c * 2 + s) * KS + k] = v; };
+
+    double2 v = make_double2(0, 0);
+    double qlen = 1;
+    if (ok)
+        for (int c = c1 - 1; c >= c0; --c) {
+            v = cfma(q, v, at(a.ULS, c));
+            qlen *= q;
+        }
+    agg[wv][lane] = v;
+    qlen_s[wv][lane] = qlen;
+    __syncthreads();
+    double2 vin = make_double2(0, 0);
+    for (int g = W - 1; g > wv; --g) vin = cfma(qlen_s[g][lane], vin, agg[g][lane]);
+    __syncthreads();
+
+    double2 bsum = make_double2(0, 0);
+    double wq = 1;
+    v = vin;
+    if (ok)
+        for (int c = c1 - 1; c >= c0; --c) {
+            put(a.UIN, c, v);
+            const double2 wt = cfma(gam, v, at(a.WLS, c));
+            bsum = cfma(wq, wt, bsum);
+            wq *= q;
+            v = cfma(q, v, at(a.ULS, c));
+        }
+    if (wv == 0 && ok) {
+        reinterpret_cast<double2 *>(a.rec + rec_AU(KS))[s * KS + k] = v;
+        if (s == 0) {
+            reinterpret_cast<double2 *>(a.rec + rec_ULS0(KS))[k] = at(a.ULS, 0);
+            reinterpret_cast<double2 *>(a.rec + rec_UIN0(KS))[k] = at(a.UIN, 0);
+        }
+    }
+    agg[wv][lane] = bsum;
+    __syncthreads();
+    double2 win = make_double2(0, 0);
+    for (int g = 0; g < wv; ++g) win = cfma(qlen_s[g][lane], win, agg[g][lane]);
+
+    double2 w = win;
+    if (ok)
+        for (int c = c0; c < c1; ++c) {
+            put(a.WIN, c, w);
+            const double2 wt = cfma(gam, at(a.UIN, c), at(a.WLS, c));
+            w = cfma(q, w, wt);
+        }
+    if (wv == W - 1 && ok) reinterpret_cast<double2 *>(a.rec + rec_AW(KS))[s * KS + k] = w;
+    if (blockIdx.x == 0 && s == 0 && threadIdx.x == 0) {
+        double d = 0;
+        for (int c = 0; c < Nc; ++c) d += a.dcpart[c];
+        a.rec[rec_DSUM(KS)] = d;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// pin: cross-rank / periodic carries, delta, singular Poisson line, pin value.  One
+// workgroup; every rank runs it redundantly on the gathered records (same order -> same
+// bits everywhere).
+// ------------------------------------------------------------------------------------
+__device__ double block_sum(double v, double *red) {  // fixed-order tree reduction
+    const int t = threadIdx.x;
+    red[t] = v;
+    __syncthreads();
+    for (int o = PIN_THREADS / 2; o > 0; o >>= 1) {
+        if (t < o) red[t] += red[t + o];
+        __syncthreads();
+    }
+    const double r = red[0];
+    __syncthreads();
+    return r;
+}
+
+__device__ double block_exscan(double v, double *red) {  // exclusive prefix sum, fixed order
+    const int t = threadIdx.x;
+    red[t] = v;
+    __syncthreads();
+    for (int o = 1; o < PIN_THREADS; o <<= 1) {
+        const double add = t >= o ? red[t - o] : 0.0;
+        __syncthreads();
+        red[t] += add;
+        __syncthreads();
+    }
+    const double incl = red[t];
+    __syncthreads();
+    return incl - v;
+}
+
+__global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
+    __shared__ double red[PIN_THREADS];
+    const int t = threadIdx.x;
+    const int G = a.nranks, KS = a.KS, KH = a.KH;
+    const int64_t Pl = a.P, Pt = a.P_total;
+    const int64_t RS = a.rec_stride;
+    auto rec = [&](int g) { return a.grec + (int64_t)g * RS; };
+
+    double delta = 0;
+    if (a.pinned0) {
+        for (int g = 0; g < G; ++g) delta += rec(g)[rec_DSUM(KS)];
+        delta = -delta;
+    }
+
+    double pin_part = 0;
+    for (int idx = t; idx < 2 * KH; idx += PIN_THREADS) {
+        const int s = idx / KH, k = idx - s * KH;
+        const Coef cf = a.coef[s * KS + k];
+        double2 *Ue = a.EXT + (size_t)s * KS + k;
+        double2 *We = a.EXT + (size_t)(2 + s) * KS + k;
+        if (s == 0 && a.pinned0 && k == 0) {
+            *Ue = make_double2(0, 0);
+            *We = make_double2(0, 0);
+            continue;
+        }
+        const bool dl = (s == 0 && a.pinned0);
+        const double rPl1 = exp((double)(Pl - 1) * cf.lr);
+        auto AU = [&](int g) {
+            double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AU(KS))[s * KS + k];
+            if (dl && g == 0) v.x += delta;
+            return v;
+        };
+        auto AW = [&](int g) {
+            double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AW(KS))[s * KS + k];
+            if (dl && g == 0) v.x += rPl1 * delta;
+            return v;
+        };
+        auto Uext = [&](int g) {  // u_true at the start of rank g+1 (ring)
+            double2 acc = make_double2(0, 0);
+            for (int m = G - 1; m >= 0; --m) acc = cfma(cf.rP, acc, AU((g + 1 + m) % G));
+            return cscale(acc, cf.inv1mrPt);
+        };
+        auto Wext = [&](int g) {  // w_true at the end of rank g-1 (ring)
+            double2 acc = make_double2(0, 0);
+            for (int m = G - 1; m >= 0; --m) {
+                const int gg = ((g - 1 - m) % G + G) % G;
+                acc = cfma(cf.rP, acc, cfma(cf.gamP, Uext(gg), AW(gg)));
+            }
+            return cscale(acc, cf.inv1mrPt);
+        };
+        const double2 ue = Uext(a.rank), we = Wext(a.rank);
+        *Ue = ue;
+        *We = we;
+        if (dl && k >= 1) {  // pinning value: rank 0, chunk 0, row 0
+            const double2 ue0 = a.rank == 0 ? ue : Uext(0);
+            const double2 we0 = a.rank == 0 ? we : Wext(0);
+            double2 u0 = reinterpret_cast<const double2 *>(rec(0) + rec_ULS0(KS))[k];
+            u0.x += delta;
+            const double2 uin0 = cfma(exp((double)(a.Nc - 1) * a.L * cf.lr), ue0,
+                                      reinterpret_cast<const double2 *>(rec(0) + rec_UIN0(KS))[k]);
+            const double2 w0 = cfma(cf.r, we0, cfma(cf.q, uin0, u0));
+            const double X = cf.cs * w0.x;
+            pin_part += (2 * k == a.M) ? X : 2 * X;
+        }
+    }
+    const double pin = block_sum(pin_part, red);
+
+    if (a.pinned0) {  // singular k = 0 Poisson line over the global y extent
+        const int64_t n = Pt;
+        const int64_t len = (n + PIN_THREADS - 1) / PIN_THREADS;
+        const int64_t b0 = min((int64_t)t * len, n), b1 = min(b0 + len, n);
+        auto h = [&](int64_t jg) {
+            const int g = (int)(jg / Pl);
+            double v = rec(g)[rec_HLINE(KS) + (jg - (int64_t)g * Pl)];
+            if (jg == 0) v += delta;
+            return v;
+        };
+        double sh = 0;
+        for (int64_t j = b0; j < b1; ++j) sh += h(j);
+        double run = block_exscan(sh, red);
+        double sS = 0;
+        for (int64_t j = b0; j < b1; ++j) {
+            run += h(j);
+            a.work[j] = run;  // S_j (inclusive)
+            sS += run;
+        }
+        const double meanS = block_sum(sS, red) / (double)n;
+        double sD = 0;
+        for (int64_t j = b0; j < b1; ++j) sD += a.work[j] - meanS;
+        double X = block_exscan(sD, red);  // X_j = sum_{i<j} (S_i - meanS)
+        const double scale = (a.dx * a.dx) / (double)a.M;
+        const int64_t lo = (int64_t)a.rank * Pl;
+        for (int64_t j = b0; j < b1; ++j) {
+            if (j >= lo && j < lo + Pl) a.line[j - lo] = scale * X;
+            X += a.work[j] - meanS;
+        }
+    }
+    if (t == 0) {
+        a.scal[0] = delta;
+        a.scal[1] = a.pinned0 ? pin : 0.0;
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// pass B: forward filter with carries, inverse row DFT, pin, back-projection, store
+// ------------------------------------------------------------------------------------
+template <int N>
+__global__ __launch_bounds__(Geo<N>::T) void spec_passB(SpecArgs a) {
+    using G = Geo<N>;
+    constexpr int T = G::T, KH = G::KH, KQ = G::KQ, EP = G::EP;
+    extern __shared__ double2 buf[];
+    const int t = threadIdx.x, c = blockIdx.x;
+    const int L = a.L, s0 = c * L, e = s0 + L - 1;
+    const int KS = a.KS;
+    const int64_t Pl = a.P, ld = a.ld;
+    const double delta = a.scal[0], pin = a.scal[1];
+    const bool inject = a.pinned0 && a.rank == 0;
+
+    double2 uin[KQ][2], w[KQ][2];
+    double pw[KQ][2];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+        const int k = t + q * T;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            uin[q][s] = make_double2(0, 0);
+            w[q][s] = make_double2(0, 0);
+            pw[q][s] = 0;
+            if ((KH % T == 0 || k < KH) && !(s == 0 && a.pinned0 && k == 0)) {
+                const Coef cf = a.coef[s * KS + k];
+                const double2 Ue = a.EXT[(size_t)s * KS + k], We = a.EXT[(size_t)(2 + s) * KS + k];
+                const int64_t n = (int64_t)c * L;
+                uin[q][s] = cfma(exp((double)(a.Nc - 1 - c) * L * cf.lr), Ue, a.UIN[((size_t)c * 2 + s) * KS + k]);
+                double gc = 0;
+                if (n > 0) gc = exp((double)(Pl - n + 1) * cf.lr) * (expm1(2.0 * n * cf.lr) / expm1(2.0 * cf.lr));
+                double2 wi = cfma(gc, Ue, a.WIN[((size_t)c * 2 + s) * KS + k]);
+                wi = cfma(exp((double)n * cf.lr), We, wi);
+                if (s == 0 && inject && c >= 1) wi.x += exp((double)(n - 1) * cf.lr) * delta;
+                w[q][s] = wi;
+                pw[q][s] = cf.q;
+            }
+        }
+    }
+
+    for (int j = s0; j <= e; ++j) {
+        const double2 *Urow = a.U + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+            const int k = t + q * T;
+            if (KH % T == 0 || k < KH) {
+                double2 X[2];
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    if (s == 0 && a.pinned0 && k == 0) {
+                        X[s] = make_double2(a.line[j], 0);
+                    } else {
+                        const Coef *cf = a.coef + s * KS + k;
+                        double2 ul = Urow[s * KS + k];
+                        if (s == 0 && inject && j == 0) ul.x += delta;
+                        const double2 ut = cfma(pw[q][s], uin[q][s], ul);
+                        w[q][s] = cfma(cf->r, w[q][s], ut);
+                        pw[q][s] *= cf->rinv;
+                        X[s] = cscale(w[q][s], cf->cs);
+                    }
+                }
+                buf[k] = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
+                if (k != 0 && 2 * k != N) buf[N - k] = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
+            }
+        }
+        __syncthreads();
+        fft_lds<N, T, true>(buf, a.tw);
+#pragma unroll
+        for (int p = 0; p < EP; ++p) {
+            const int i = t + p * T;
+            if (N % T == 0 || i < N) {
+                const double2 z = buf[i];
+                const double x1 = z.x - pin, x2 = z.y;
+                const double o1 = a.pin_out[0] * x1 + a.pin_out[1] * x2;
+                store_with_ghosts(a.out1, ld, N, Pl, i, j, o1, a.write_ghost_rows);
+                if (a.out2) {
+                    const double o2 = a.pin_out[2] * x1 + a.pin_out[3] * x2;
+                    store_with_ghosts(a.out2, ld, N, Pl, i, j, o2, a.write_ghost_rows);
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------
+template <int N>
+static int launch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
+    const size_t lds = sizeof(double2) * N;
+    if (passB) {
+        QG_HIP(hipFuncSetAttribute((const void *)spec_passB<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        spec_passB<N><<<a.Nc, Geo<N>::T, lds, s>>>(a);
+    } else {
+        QG_HIP(hipFuncSetAttribute((const void *)spec_passA<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        spec_passA<N><<<a.Nc, Geo<N>::T, lds, s>>>(a);
+    }
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
+    switch (a.M) {
+        case 8: return launch_pass<8>(passB, a, s);
+        case 16: return launch_pass<16>(passB, a, s);
+        case 32: return launch_pass<32>(passB, a, s);
+        case 64: return launch_pass<64>(passB, a, s);
+        case 128: return launch_pass<128>(passB, a, s);
+        case 256: return launch_pass<256>(passB, a, s);
+        case 512: return launch_pass<512>(passB, a, s);
+        case 1024: return launch_pass<1024>(passB, a, s);
+        case 2048: return launch_pass<2048>(passB, a, s);
+        case 4096: return launch_pass<4096>(passB, a, s);
+        default: return QG_ERR_UNSUPPORTED;
+    }
+}
+
+bool SpectralSolver::supports(int64_t M, int64_t P) {
+    return M >= 8 && M <= 4096 && (M & (M - 1)) == 0 && P >= 2;
+}
+
+static int pick_chunk(int64_t P, int req) {
+    if (req > 0) return (P % req == 0) ? req : -1;
+    for (int L = 16; L >= 1; L >>= 1)
+        if (P % L == 0) return L;
+    return 1;
+}
+
+static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks, double dx,
+                         const double alpha[2], int pinned0, const double pin_in[4], const double pin_out[4],
+                         int chunk_rows) {
+    if (!supports(M, P)) return QG_ERR_UNSUPPORTED;
+    if (!(dx > 0) || nranks < 1 || rank < 0 || rank >= nranks || P_total != P * nranks) return QG_ERR_INVALID_ARG;
+    const int L = pick_chunk(P, chunk_rows);
+    if (L < 1) return QG_ERR_INVALID_ARG;
+    SpecArgs &a = a_;
+    a.M = M;
+    a.P = P;
+    a.ld = M + 2;
+    a.P_total = P_total;
+    a.rank = rank;
+    a.nranks = nranks;
+    a.L = L;
+    a.Nc = (int)(P / L);
+    a.KH = (int)(M / 2 + 1);
+    a.KS = (a.KH + 63) & ~63;
+    a.dx = dx;
+    a.pinned0 = pinned0 ? 1 : 0;
+    std::memcpy(a.pin_in, pin_in, sizeof(a.pin_in));
+    std::memcpy(a.pin_out, pin_out, sizeof(a.pin_out));
+    const int KS = a.KS;
+
+    // ---- tables (long double) --------------------------------------------------------
+    std::vector<double2> tw(M);
+    const long double twopi = 6.283185307179586476925286766559L;
+    for (int64_t m = 0; m < M; ++m) {
+        const long double ang = twopi * (long double)m / (long double)M;
+        tw[m] = make_double2((double)cosl(ang), (double)-sinl(ang));
+    }
+    std::vector<Coef> coef(2 * (size_t)KS);
+    std::memset(coef.data(), 0, sizeof(Coef) * coef.size());
+    for (int s = 0; s < 2; ++s)
+        for (int k = 0; k < a.KH; ++k) {
+            Coef &cf = coef[s * KS + k];
+            if (s == 0 && pinned0 && k == 0) continue;  // singular line, r = 0 marker
+            const long double th = twopi * (long double)k / (long double)M;
+            const long double sh = sinl(th / 2);
+            const long double d = 2 * sh * sh - (long double)alpha[s] * (long double)dx * (long double)dx / 2;
+            if (!(d > 0)) return QG_ERR_UNSUPPORTED;  // singular (alpha = 0 unpinned) or alpha > 0
+            // r = rho - sqrt(rho^2 - 1) with rho = 1 + d, in cancellation-free form
+            const long double sq = sqrtl(d * (d + 2));
+            const long double r = 1 / ((1 + d) + sq);
+            const long double lr = -log1pl(d + sq);
+            if (!(r > 1e-300L)) return QG_ERR_UNSUPPORTED;  // |alpha| dx^2 beyond double range
+            cf.r = (double)r;
+            cf.rinv = (double)(1 / r);
+            cf.lr = (double)lr;
+            cf.q = (double)expl(L * lr);
+            cf.gam = (double)(r * expm1l(2 * L * lr) / expm1l(2 * lr));
+            cf.rP = (double)expl((long double)P * lr);
+            cf.gamP = (double)(r * expm1l(2 * (long double)P * lr) / expm1l(2 * lr));
+            cf.cs = (double)(-r * (long double)dx * (long double)dx / (long double)M);
+            cf.inv1mrPt = (double)(-1 / expm1l((long double)P_total * lr));
+        }
+
+    // ---- device memory ---------------------------------------------------------------
+    const size_t n_tw = align_up(sizeof(double2) * M);
+    const size_t n_coef = align_up(sizeof(Coef) * coef.size());
+    const size_t n_U = align_up(sizeof(double2) * (size_t)P * 2 * KS);
+    const size_t n_S = align_up(sizeof(double2) * (size_t)a.Nc * 2 * KS);
+    const size_t n_dc = align_up(sizeof(double) * a.Nc);
+    const int64_t RS = rec_size(KS, P);
+    const size_t n_rec = align_up(sizeof(double) * RS);
+    const size_t n_grec = nranks > 1 ? align_up(sizeof(double) * RS * nranks) : 0;
+    const size_t n_ext = align_up(sizeof(double2) * 4 * KS);
+    const size_t n_line = align_up(sizeof(double) * P);
+    const size_t n_scal = align_up(sizeof(double) * 8);
+    const size_t n_work = align_up(sizeof(double) * P_total);
+    bytes_ = n_tw + n_coef + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + n_line + n_scal + n_work;
+    if (hipMalloc(&mem_, bytes_) != hipSuccess) {
+        mem_ = nullptr;
+        return QG_ERR_ALLOC;
+    }
+    char *p = static_cast<char *>(mem_);
+    auto take = [&](size_t n) { char *r = p; p += n; return r; };
+    double2 *d_tw = (double2 *)take(n_tw);
+    Coef *d_coef = (Coef *)take(n_coef);
+    a.U = (double2 *)take(n_U);
+    a.ULS = (double2 *)take(n_S);
+    a.WLS = (double2 *)take(n_S);
+    a.UIN = (double2 *)take(n_S);
+    a.WIN = (double2 *)take(n_S);
+    a.dcpart = (double *)take(n_dc);
+    a.rec = (double *)take(n_rec);
+    grec_buf_ = nranks > 1 ? (double *)take(n_grec) : nullptr;
+    a.grec = nranks > 1 ? grec_buf_ : a.rec;
+    a.rec_stride = RS;
+    a.EXT = (double2 *)take(n_ext);
+    a.line = (double *)take(n_line);
+    a.scal = (double *)take(n_scal);
+    a.work = (double *)take(n_work);
+    a.tw = d_tw;
+    a.coef = d_coef;
+    QG_HIP(hipMemcpy(d_tw, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice));
+    QG_HIP(hipMemcpy(d_coef, coef.data(), sizeof(Coef) * coef.size(), hipMemcpyHostToDevice));
+    QG_HIP(hipMemset(a.rec, 0, n_rec));
+    QG_HIP(hipMemset(a.scal, 0, n_scal));
+    QG_HIP(hipMemset(a.line, 0, n_line));
+    return QG_OK;
+}
+
+SpectralSolver::~SpectralSolver() {
+    if (mem_) (void)hipFree(mem_);
+}
+
+int SpectralSolver::solve(const double *in1, const double *in2, double *out1, double *out2, int write_ghost_rows,
+                          hipStream_t s, GatherFn gather, void *user) {
+    if (!mem_) return QG_ERR_NOT_BOUND;
+    SpecArgs a = a_;
+    a.in1 = in1;
+    a.in2 = in2 ? in2 : in1;
+    a.out1 = out1;
+    a.out2 = out2;
+    a.write_ghost_rows = write_ghost_rows;
+    QG_CHECK(dispatch_pass(false, a, s));
+    spec_carry<<<dim3((unsigned)((a.KH + 63) / 64), 2), 64 * CARRY_WAVES, 0, s>>>(a);
+    QG_LAUNCH_CHECK();
+    if (a.nranks > 1) {
+        if (!gather) return QG_ERR_RCCL;
+        QG_CHECK(gather(user, a.rec, grec_buf_, a.rec_stride, s));
+    }
+    spec_pin<<<1, PIN_THREADS, 0, s>>>(a);
+    QG_LAUNCH_CHECK();
+    QG_CHECK(dispatch_pass(true, a, s));
+    return QG_OK;
+}
+
+}  // namespace qg

@@ -1,0 +1,90 @@
+// Direct periodic 5-point solver for the pair of systems of evolve_psi! (Poisson, pinned;
+// modified Helmholtz), replacing the two CHOLMOD factors (src/schemes/laplacian.jl:60-75,
+// solves at src/model.jl:186,191).
+//
+// Method (FACR(0): Fourier in x, tridiagonal in y):
+//   1. pass A   one workgroup per chunk of L rows.  Each row of the two right-hand sides is
+//               projected, packed as z = f1 + i f2, DFT'd in LDS, split into the two
+//               half-spectra; every wavenumber k then runs the backward first-order filter
+//               u_j = F_j + r_k u_{j+1} of the cyclic tridiagonal line solve
+//               X_{j-1} - 2 rho_k X_j + X_{j+1} = dx^2 F_j (factored as (1-rS)(1-rS^-1)),
+//               chunk-local (zero carry).  Writes u (the only full-size intermediate) and two
+//               complex chunk summaries per (system, k).
+//   2. carry    segment-parallel scans over chunks -> chunk carry-ins (local to this rank)
+//               and rank aggregates.
+//   3. [RCCL all-gather of the rank records when the y direction is split over GPUs]
+//   4. pin      one workgroup: cross-rank carries, Poisson compatibility shift delta, the
+//               singular k = 0 Poisson line (double prefix sum), the pinning value.
+//   5. pass B   one workgroup per chunk: forward filter w_j = u_true_j + r w_{j-1} with the
+//               carries, X = -r dx^2 w / M, inverse DFT in LDS, pin, back-projection, store
+//               with the ghost ring.
+// HBM traffic per grid point for both systems: read 2 + write 2 (pass A), read 2 + write 2
+// (pass B) doubles, plus ~0.5 double of chunk summaries.
+#pragma once
+
+#include "qg_common.hpp"
+
+namespace qg {
+
+struct Coef {  // per (system, k); see SpectralSolver::build_tables
+    double r, rinv, lr, q, gam, rP, gamP, cs, inv1mrPt, pad;
+};
+
+struct SpecArgs {
+    int64_t M, P, ld;         // M = row length (power of two), P = local rows, ld = M + 2
+    int64_t P_total;          // global rows
+    int rank, nranks;
+    int L, Nc, KH, KS;        // chunk rows, chunks, M/2+1, padded k stride
+    double dx;
+    int pinned0;              // system 0 is the pinned Poisson problem
+    double pin_in[4];         // projection of the inputs
+    double pin_out[4];        // back-projection of the outputs
+    int write_ghost_rows;
+    const double *in1, *in2;  // (M+2, P+2) fields
+    double *out1, *out2;
+    const double2 *tw;        // M twiddles
+    const Coef *coef;         // [2][KS]
+    double2 *U;               // [P][2][KS]
+    double2 *ULS, *WLS;       // [Nc][2][KS]
+    double2 *UIN, *WIN;       // [Nc][2][KS]
+    double *dcpart;           // [Nc]
+    double *rec;              // this rank's record (see rec_* offsets)
+    const double *grec;       // gathered records [nranks] (== rec when nranks == 1)
+    int64_t rec_stride;       // doubles per record
+    double2 *EXT;             // [2 (Uext, Wext)][2][KS]
+    double *line;             // [P] local segment of the singular line (already / M)
+    double *scal;             // [0] = delta, [1] = pin
+    double *work;             // pin-kernel scratch: >= P_total doubles
+};
+
+// record layout (doubles)
+__host__ __device__ inline int64_t rec_AU(int KS) { return 0; }                 // [2][KS] double2
+__host__ __device__ inline int64_t rec_AW(int KS) { return 4 * (int64_t)KS; }  // [2][KS] double2
+__host__ __device__ inline int64_t rec_ULS0(int KS) { return 8 * (int64_t)KS; }  // [KS] double2 (sys 0)
+__host__ __device__ inline int64_t rec_UIN0(int KS) { return 10 * (int64_t)KS; } // [KS] double2 (sys 0)
+__host__ __device__ inline int64_t rec_DSUM(int KS) { return 12 * (int64_t)KS; } // 2 doubles
+__host__ __device__ inline int64_t rec_HLINE(int KS) { return 12 * (int64_t)KS + 2; }  // [P]
+__host__ __device__ inline int64_t rec_size(int KS, int64_t P) { return 12 * (int64_t)KS + 2 + ((P + 1) & ~1LL); }
+
+class SpectralSolver {
+public:
+    // alpha[s]: construct_spA shift; pinned0: system 0 is the pinned Poisson problem
+    int init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks, double dx, const double alpha[2],
+             int pinned0, const double pin_in[4], const double pin_out[4], int chunk_rows);
+    ~SpectralSolver();
+    static bool supports(int64_t M, int64_t P);
+    // enqueue the whole solve; `gather` (may be null) all-gathers rec -> grec across ranks
+    typedef int (*GatherFn)(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
+    int solve(const double *in1, const double *in2, double *out1, double *out2, int write_ghost_rows,
+              hipStream_t s, GatherFn gather = nullptr, void *user = nullptr);
+    const SpecArgs &args() const { return a_; }
+    size_t device_bytes() const { return bytes_; }
+
+private:
+    SpecArgs a_{};
+    void *mem_ = nullptr;
+    double *grec_buf_ = nullptr;
+    size_t bytes_ = 0;
+};
+
+}  // namespace qg

@@ -1,0 +1,19 @@
+"""qgamd -- MI355X-native two-layer Phillips (baroclinic QG) hot path.
+
+Host mirror of the reference's operator surface (src/model.jl, src/schemes/*.jl,
+src/run_model_no_output.jl of JSLeadbetter/julia-ocean-modelling) over the HIP C-ABI in
+include/qg_mi355.h.  See model.py for the mapping.
+"""
+from . import _lib
+from ._lib import LIB_PATH, QGError, lib
+from .model import *  # noqa: F401,F403
+from .model import (BaroclinicModel, PairSolver, State, bench_model, cd, device_zeros,
+                    evolve_psi_, evolve_zeta_, get_helmholtz_cholesky, get_poisson_cholesky,
+                    initialise_model, J, laplace_5p, make_model, run_model_no_output,
+                    sp_solve_modified_helmholtz, sp_solve_poisson, update_doubly_periodic_bc_)
+
+__all__ = ["BaroclinicModel", "PairSolver", "State", "bench_model", "cd", "device_zeros",
+           "evolve_psi_", "evolve_zeta_", "get_helmholtz_cholesky", "get_poisson_cholesky",
+           "initialise_model", "J", "laplace_5p", "make_model", "run_model_no_output",
+           "sp_solve_modified_helmholtz", "sp_solve_poisson", "update_doubly_periodic_bc_",
+           "LIB_PATH", "QGError", "lib"]

@@ -1,0 +1,108 @@
+"""ctypes binding of lib/libqgmi355.so (the C-ABI declared in include/qg_mi355.h).
+
+There is no fallback: if the HIP library is missing or fails to load, every entry point
+raises.  The parity tests rely on that (a CPU fallback would void them).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libqgmi355.so")
+
+QG_OK = 0
+QG_SOLVER_SPECTRAL = 0
+QG_SOLVER_PCG = 1
+QG_PRECOND_NONE = 0
+QG_PRECOND_SPECTRAL = 1
+
+
+class QgParams(C.Structure):
+    """Mirror of ``struct qg_params`` (field order and types must match the header)."""
+
+    _fields_ = [
+        ("H_1", C.c_double), ("H_2", C.c_double), ("beta", C.c_double), ("Lx", C.c_double),
+        ("Ly", C.c_double), ("dt", C.c_double), ("T", C.c_double), ("U", C.c_double),
+        ("M", C.c_int64), ("P", C.c_int64),
+        ("dx", C.c_double), ("visc", C.c_double), ("r", C.c_double), ("R_d", C.c_double),
+        ("initial_kick", C.c_double),
+        ("P_fwd", C.c_double * 4),
+        ("solver", C.c_int32), ("precond", C.c_int32),
+        ("pcg_rtol", C.c_double),
+        ("pcg_maxit", C.c_int32), ("chunk_rows", C.c_int32),
+    ]
+
+
+class QgStats(C.Structure):
+    _fields_ = [("iters", C.c_int32 * 2), ("relres", C.c_double * 2), ("delta", C.c_double),
+                ("pin", C.c_double)]
+
+
+# (name, restype, argtypes) of every symbol include/qg_mi355.h declares
+_vp, _dp, _i64, _i32 = C.c_void_p, C.c_void_p, C.c_int64, C.c_int
+SIGNATURES = [
+    ("qg_abi_version", C.c_int, []),
+    ("qg_strerror", C.c_char_p, [C.c_int]),
+    ("qg_default_params", None, [C.POINTER(QgParams)]),
+    ("qg_create", C.c_int, [C.POINTER(QgParams), C.c_int, _vp, C.POINTER(_vp)]),
+    ("qg_destroy", C.c_int, [_vp]),
+    ("qg_bind_state", C.c_int, [_vp, _dp, _dp, _dp]),
+    ("qg_initialise", C.c_int, [_vp, C.c_uint64, C.c_uint64]),
+    ("qg_evolve_zeta", C.c_int, [_vp, _i64]),
+    ("qg_evolve_psi", C.c_int, [_vp]),
+    ("qg_step", C.c_int, [_vp, _i64]),
+    ("qg_run", C.c_int, [_vp, _i64, _i64]),
+    ("qg_slot", C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_int)]),
+    ("qg_set_slots", C.c_int, [_vp, C.c_int * 3]),
+    ("qg_canonicalize", C.c_int, [_vp]),
+    ("qg_get_stats", C.c_int, [_vp, C.POINTER(QgStats)]),
+    ("qg_synchronize", C.c_int, [_vp]),
+    ("qg_comm_unique_id", C.c_int, [C.c_char_p]),
+    ("qg_comm_init", C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
+    ("qg_solver_create", C.c_int, [_i64, _i64, C.c_double, C.c_double * 2, C.c_int * 2,
+                                   C.c_double * 4, C.c_double * 4, C.c_int, C.c_int, C.c_int, _vp,
+                                   C.POINTER(_vp)]),
+    ("qg_solver_solve", C.c_int, [_vp, _dp, _dp, _dp, _dp]),
+    ("qg_solver_destroy", C.c_int, [_vp]),
+    ("qg_laplace_5p", C.c_int, [_dp, _dp, _i64, _i64, C.c_double, _vp]),
+    ("qg_cd", C.c_int, [_dp, _dp, _i64, _i64, C.c_double, _vp]),
+    ("qg_arakawa_J", C.c_int, [_dp, _dp, _dp, _i64, _i64, C.c_double, _vp]),
+    ("qg_fill_ghosts", C.c_int, [_dp, _i64, _i64, _vp]),
+]
+
+_lib = None
+
+
+class QGError(RuntimeError):
+    def __init__(self, fn, status):
+        msg = _lib.qg_strerror(status).decode() if _lib is not None else str(status)
+        super().__init__(f"{fn} failed with status {status}: {msg}")
+        self.status = status
+
+
+def lib():
+    """Load the HIP library (raises if it is not built -- there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} not found: build it with `make -C julia-ocean-modelling_amd` "
+                "(or __graft_entry__.build()); the QG hot path has no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(fn, status):
+    if status != QG_OK:
+        raise QGError(fn, status)
+    return status
+
+
+def call(name, *args):
+    return check(name, getattr(lib(), name)(*args))

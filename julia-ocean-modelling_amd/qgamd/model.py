@@ -1,0 +1,384 @@
+"""Host-side mirror of the reference's operator surface for the hot path, driving the HIP
+C-ABI (include/qg_mi355.h) on device arrays.
+
+Reference surface (JSLeadbetter/julia-ocean-modelling, paths relative to its root):
+  BaroclinicModel + outer constructor          src/model.jl:12-34
+  ratio_term, S1_plus, S2_minus, beta_1/2, S_eig  src/model.jl:109-121
+  P_matrix, P_inv_matrix                        src/model.jl:83-99
+  initialise_model                              src/model.jl:37-62
+  evolve_zeta!, evolve_psi!                     src/model.jl:155-199
+  get_poisson_cholesky, get_helmholtz_cholesky  src/schemes/laplacian.jl:60-75
+  run_model_no_output                           src/run_model_no_output.jl:3-16
+  laplace_5p, cd, J, update_doubly_periodic_bc! laplacian.jl:15, model.jl:68, arakawa.jl:58,
+                                                boundary_conditions.jl:2
+  sp_solve_modified_helmholtz, sp_solve_poisson laplacian.jl:78-111
+
+Device arrays are torch float64 CUDA tensors used only as memory: a Julia
+(M+2, P+2, 2, 3) column-major array is a C-contiguous tensor of shape (3, 2, P+2, M+2)
+(``[slot, layer, j, i]``), a Julia (M+2, P+2) matrix a (P+2, M+2) tensor.  Python names
+cannot carry ``!``; the mutating functions end in ``_`` instead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import _lib
+from ._lib import QgParams, QgStats, call
+
+MINUTES = 60
+DAY = 60 * 60 * 24
+KM = 1000.0
+YEAR = 60 * 60 * 24 * 365
+
+SEED_LAYER1 = 20241008
+SEED_LAYER2 = 20241009
+
+
+# ---------------------------------------------------------------------------------------
+# parameters
+# ---------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class BaroclinicModel:
+    """``struct BaroclinicModel`` (src/model.jl:12-30).  Build with :func:`make_model`
+    (the outer constructor, model.jl:33-34) or :meth:`create`."""
+
+    H_1: float
+    H_2: float
+    H: float
+    beta: float
+    Lx: float
+    Ly: float
+    dt: float
+    T: float
+    U: float
+    M: int
+    P: int
+    dx: float
+    visc: float
+    r: float
+    R_d: float
+    initial_kick: float
+
+    @staticmethod
+    def create(H_1, H_2, beta, Lx, Ly, dt, T, U, M, P, dx, visc, r, R_d, initial_kick):
+        return make_model(H_1, H_2, beta, Lx, Ly, dt, T, U, M, P, dx, visc, r, R_d, initial_kick)
+
+
+def make_model(H_1, H_2, beta, Lx, Ly, dt, T, U, M, P, dx, visc, r, R_d, initial_kick):
+    """Outer constructor (model.jl:33-34): H = H_1 + H_2."""
+    return BaroclinicModel(float(H_1), float(H_2), float(H_1) + float(H_2), float(beta), float(Lx),
+                           float(Ly), float(dt), float(T), float(U), int(M), int(P), float(dx),
+                           float(visc), float(r), float(R_d), float(initial_kick))
+
+
+def bench_model(N, dt=30.0 * MINUTES, T=1.0 * DAY, P=None, Lx=4000.0 * KM):
+    """Benchmark parameter set of src/benchmarking/julia_bench_parts.jl:6-18 (square cells)."""
+    P = N if P is None else P
+    return make_model(1.0 * KM, 2.0 * KM, 2e-11, Lx, Lx * P / N, dt, T, 0.1, N, P, Lx / N, 100.0,
+                      1e-7, 40.0 * KM, 1e-6)
+
+
+def ratio_term(m):  # model.jl:109-111
+    return 0.5 * (m.H_1 + m.H_2) / ((m.R_d * m.R_d) * ((1 / m.H_1) + (1 / m.H_2)))
+
+
+def S1_plus(m):  # model.jl:113
+    return (2 * ratio_term(m)) / (m.H_1 * (m.H_1 + m.H_2))
+
+
+def S2_minus(m):  # model.jl:114
+    return (2 * ratio_term(m)) / (m.H_2 * (m.H_1 + m.H_2))
+
+
+def beta_1(m):  # model.jl:117
+    return m.beta + (S1_plus(m) * m.U)
+
+
+def beta_2(m):  # model.jl:118
+    return m.beta - (S2_minus(m) * m.U)
+
+
+def S_eig(m):  # model.jl:121
+    return -1 / (m.R_d * m.R_d)
+
+
+def P_matrix(H_1, H_2):  # model.jl:83-87
+    P = np.ones((2, 2))
+    P[0, 1] = -H_2 / H_1
+    return P
+
+
+def P_inv_matrix(m):  # model.jl:90-99
+    a, b = S1_plus(m), S2_minus(m)
+    return (1 / (a + b)) * np.array([[b, a], [-b, b]])
+
+
+def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_local=None):
+    p = QgParams()
+    _lib.lib().qg_default_params(C.byref(p))
+    for n in ("H_1", "H_2", "beta", "Lx", "Ly", "dt", "T", "U", "dx", "visc", "r", "R_d",
+              "initial_kick"):
+        setattr(p, n, float(getattr(m, n)))
+    p.M = int(m.M)
+    p.P = int(m.P if P_local is None else P_local)
+    if P_fwd is not None:
+        for k, v in enumerate(np.asarray(P_fwd, dtype=np.float64).reshape(-1)):
+            p.P_fwd[k] = float(v)
+    p.solver = int(solver)
+    p.chunk_rows = int(chunk_rows)
+    return p
+
+
+# ---------------------------------------------------------------------------------------
+# device plumbing
+# ---------------------------------------------------------------------------------------
+def _torch():
+    import torch
+    return torch
+
+
+def _stream_ptr():
+    torch = _torch()
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr())
+
+
+def _check_field(t, M, P):
+    torch = _torch()
+    if not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()):
+        raise ValueError("expected a contiguous float64 CUDA tensor")
+    if tuple(t.shape[-2:]) != (P + 2, M + 2):
+        raise ValueError(f"field shape {tuple(t.shape)} does not match (P+2, M+2) = {(P + 2, M + 2)}")
+
+
+def device_zeros(m, P_local=None, device="cuda"):
+    """zeros(M+2, P+2, 2, 3) in Julia layout -> tensor (3, 2, P+2, M+2)."""
+    torch = _torch()
+    P = m.P if P_local is None else P_local
+    return torch.zeros((3, 2, P + 2, m.M + 2), dtype=torch.float64, device=device)
+
+
+class State:
+    """The model state zeta, psi, f_store plus the library context that evolves it.
+
+    Plays the role of the reference's (zeta, psi, f_store) arrays and its two CHOLMOD
+    factors.  History slots rotate (no copies): :meth:`slot` maps the reference's slot
+    index (1 = newest) to the physical slot, :meth:`logical` returns the reference-ordered
+    view, :meth:`canonicalize` physically restores the reference order.
+    """
+
+    def __init__(self, m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0,
+                 device=None, rank=0, nranks=1, P_local=None):
+        torch = _torch()
+        self.model = m
+        self.P_local = m.P if P_local is None else P_local
+        self.device = torch.cuda.current_device() if device is None else device
+        self.zeta = device_zeros(m, self.P_local)
+        self.psi = device_zeros(m, self.P_local)
+        self.f_store = device_zeros(m, self.P_local)
+        self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local)
+        self._ctx = C.c_void_p()
+        call("qg_create", C.byref(self.params), int(self.device), _stream_ptr(), C.byref(self._ctx))
+        call("qg_bind_state", self._ctx, _ptr(self.zeta), _ptr(self.psi), _ptr(self.f_store))
+        self.rank, self.nranks = rank, nranks
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx and _lib._lib is not None:
+            _lib._lib.qg_destroy(ctx)
+            self._ctx = None
+
+    # -- multi-GPU ---------------------------------------------------------------------
+    def comm_init(self, nranks, rank, uid: bytes):
+        call("qg_comm_init", self._ctx, int(nranks), int(rank), C.c_char_p(uid))
+        self.rank, self.nranks = rank, nranks
+
+    # -- reference operations ----------------------------------------------------------
+    def initialise(self, seeds=(SEED_LAYER1, SEED_LAYER2)):
+        call("qg_initialise", self._ctx, int(seeds[0]), int(seeds[1]))
+        return self
+
+    def evolve_zeta_(self, timestep):
+        call("qg_evolve_zeta", self._ctx, int(timestep))
+
+    def evolve_psi_(self):
+        call("qg_evolve_psi", self._ctx)
+
+    def step(self, timestep):
+        call("qg_step", self._ctx, int(timestep))
+
+    def run(self, first_step, nsteps):
+        call("qg_run", self._ctx, int(first_step), int(nsteps))
+
+    def synchronize(self):
+        call("qg_synchronize", self._ctx)
+
+    def stats(self):
+        s = QgStats()
+        call("qg_get_stats", self._ctx, C.byref(s))
+        return {"delta": s.delta, "pin": s.pin, "iters": list(s.iters), "relres": list(s.relres)}
+
+    # -- slot rotation -----------------------------------------------------------------
+    def slot(self, which, logical):
+        w = {"zeta": 0, "psi": 1, "f_store": 2}[which]
+        out = C.c_int()
+        call("qg_slot", self._ctx, w, int(logical), C.byref(out))
+        return out.value
+
+    def heads(self):
+        return [self.slot(w, 1) for w in ("zeta", "psi", "f_store")]
+
+    def set_heads(self, heads):
+        call("qg_set_slots", self._ctx, (C.c_int * 3)(*[int(h) for h in heads]))
+
+    def logical(self, which):
+        """(3, 2, P+2, M+2) tensor in reference slot order (a gathered copy)."""
+        torch = _torch()
+        t = getattr(self, which)
+        order = [self.slot(which, s) for s in (1, 2, 3)]
+        return t[torch.tensor(order, device=t.device)]
+
+    def current(self, which, layer):
+        """Reference ``X[:, :, layer, 1]`` (layer 1-based) as a (P+2, M+2) view."""
+        return getattr(self, which)[self.slot(which, 1), layer - 1]
+
+    def canonicalize(self):
+        call("qg_canonicalize", self._ctx)
+
+    def to_numpy(self, which):
+        """Reference-ordered numpy array of shape (M+2, P+2, 2, 3) (Julia index order)."""
+        return self.logical(which).permute(3, 2, 1, 0).contiguous().cpu().numpy()
+
+
+# ---------------------------------------------------------------------------------------
+# the reference's free functions
+# ---------------------------------------------------------------------------------------
+def initialise_model(m, seeds=(SEED_LAYER1, SEED_LAYER2), **kw):
+    """initialise_model (model.jl:37-62) with seeded noise; returns the device State."""
+    if not np.sign(beta_1(m)) == -np.sign(beta_2(m)):  # model.jl:38
+        raise AssertionError("sign(beta_1) must equal -sign(beta_2)")
+    return State(m, **kw).initialise(seeds)
+
+
+def evolve_zeta_(m, state, timestep):
+    """evolve_zeta!(model, zeta, psi, timestep, f_store) (model.jl:155-158)."""
+    state.evolve_zeta_(timestep)
+
+
+class SolverHandle:
+    """Stands in for SparseArrays.CHOLMOD.Factor in evolve_psi!'s signature.  The state's
+    context owns the actual solver (both systems are solved together on the device)."""
+
+    def __init__(self, kind, M, P, dx, alpha):
+        self.kind, self.M, self.P, self.dx, self.alpha = kind, M, P, dx, alpha
+
+
+def get_poisson_cholesky(M, P, dx):  # laplacian.jl:66-75
+    return SolverHandle("poisson", M, P, dx, 0.0)
+
+
+def get_helmholtz_cholesky(M, P, dx, alpha):  # laplacian.jl:60-64
+    return SolverHandle("helmholtz", M, P, dx, alpha)
+
+
+def evolve_psi_(m, state, poisson=None, helmholtz=None):
+    """evolve_psi!(model, zeta, psi, poisson_cholesky, helmholtz_cholesky) (model.jl:172-199)."""
+    for h, kind in ((poisson, "poisson"), (helmholtz, "helmholtz")):
+        if h is not None and (h.kind != kind or h.M != m.M or h.P != m.P or h.dx != m.dx):
+            raise ValueError(f"{kind} handle does not match the model")
+    if helmholtz is not None and helmholtz.alpha != S_eig(m):
+        raise ValueError("helmholtz handle alpha != S_eig(model)")
+    state.evolve_psi_()
+
+
+def run_model_no_output(m, nsteps=None, seeds=(SEED_LAYER1, SEED_LAYER2), **kw):
+    """run_model_no_output.jl:3-16: init, total_steps = floor(T/dt) steps; returns State."""
+    st = initialise_model(m, seeds, **kw)
+    total = int(np.floor(m.T / m.dt)) if nsteps is None else int(nsteps)
+    st.run(1, total)
+    return st
+
+
+# ---- stateless operators on (P+2, M+2) device matrices -----------------------------------
+def _dims(u):
+    P2, M2 = u.shape[-2:]
+    return M2 - 2, P2 - 2
+
+
+def laplace_5p(u, dx):
+    torch = _torch()
+    M, P = _dims(u)
+    _check_field(u, M, P)
+    out = torch.empty_like(u)
+    call("qg_laplace_5p", _ptr(u), _ptr(out), M, P, float(dx), _stream_ptr())
+    return out
+
+
+def cd(u, dx):
+    torch = _torch()
+    M, P = _dims(u)
+    _check_field(u, M, P)
+    out = torch.empty_like(u)
+    call("qg_cd", _ptr(u), _ptr(out), M, P, float(dx), _stream_ptr())
+    return out
+
+
+def J(dx, zeta, psi):
+    torch = _torch()
+    M, P = _dims(zeta)
+    _check_field(zeta, M, P)
+    _check_field(psi, M, P)
+    out = torch.empty_like(zeta)
+    call("qg_arakawa_J", _ptr(zeta), _ptr(psi), _ptr(out), M, P, float(dx), _stream_ptr())
+    return out
+
+
+def update_doubly_periodic_bc_(b):
+    M, P = _dims(b)
+    _check_field(b, M, P)
+    call("qg_fill_ghosts", _ptr(b), M, P, _stream_ptr())
+    return b
+
+
+class PairSolver:
+    """qg_solver handle: A_s x_s = proj_in . f for s = 0 (optionally pinned Poisson), 1."""
+
+    def __init__(self, M, P, dx, alpha, pinned=(0, 0), proj_in=(1, 0, 0, 1), proj_out=(1, 0, 0, 1),
+                 kind=_lib.QG_SOLVER_SPECTRAL):
+        torch = _torch()
+        self.M, self.P = M, P
+        self._h = C.c_void_p()
+        call("qg_solver_create", int(M), int(P), float(dx), (C.c_double * 2)(*alpha),
+             (C.c_int * 2)(*pinned), (C.c_double * 4)(*proj_in), (C.c_double * 4)(*proj_out),
+             int(kind), 1, int(torch.cuda.current_device()), _stream_ptr(), C.byref(self._h))
+
+    def solve(self, f1, f2=None, out1=None, out2=None):
+        torch = _torch()
+        _check_field(f1, self.M, self.P)
+        out1 = torch.empty_like(f1) if out1 is None else out1
+        call("qg_solver_solve", self._h, _ptr(f1), _ptr(f2) if f2 is not None else None, _ptr(out1),
+             _ptr(out2) if out2 is not None else None)
+        return out1 if out2 is None else (out1, out2)
+
+    def __del__(self):
+        if getattr(self, "_h", None) and _lib._lib is not None:
+            _lib._lib.qg_solver_destroy(self._h)
+            self._h = None
+
+
+def sp_solve_modified_helmholtz(M, P, dx, f, alpha):
+    """laplacian.jl:78-86: solution x of construct_spA(M,P,dx,alpha) x = f, with ghosts."""
+    s = PairSolver(M, P, dx, (float(alpha), -1.0), (0, 0), (1, 0, 0, 0), (1, 0, 0, 0))
+    return s.solve(f)
+
+
+def sp_solve_poisson(M, P, dx, f):
+    """laplacian.jl:100-111: the pinned Poisson solve (x = 0 at interior (1,1))."""
+    s = PairSolver(M, P, dx, (0.0, -1.0), (1, 0), (1, 0, 0, 0), (1, 0, 0, 0))
+    return s.solve(f)

@@ -1,0 +1,78 @@
+"""CPU checks of the C-ABI library: it builds, loads, exports every symbol declared in
+include/qg_mi355.h, and the ctypes mirror of qg_params matches the C layout.  No compute
+calls (there is no GPU here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "julia-ocean-modelling_amd")
+HEADER = os.path.join(ROOT, "include", "qg_mi355.h")
+
+
+@pytest.fixture(scope="module")
+def qglib():
+    import qgamd
+    if not os.path.exists(qgamd.LIB_PATH):
+        subprocess.run(["make", "-s", "-C", PKG, "-j8"], check=True)
+    return qgamd.lib()
+
+
+def _declared():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char \*)\s*\*?\s*(qg_\w+)\s*\(", txt, re.M)))
+
+
+def test_exports_every_declared_symbol(qglib):
+    names = _declared()
+    assert len(names) >= 20
+    import qgamd._lib as L
+    bound = {n for n, _, _ in L.SIGNATURES}
+    for n in names:
+        assert hasattr(qglib, n), n
+        assert n in bound, f"{n} has no ctypes signature"
+
+
+def test_abi_version_and_strerror(qglib):
+    assert qglib.qg_abi_version() == 1
+    assert qglib.qg_strerror(0) == b"ok"
+    assert b"unsupported" in qglib.qg_strerror(-2)
+
+
+def test_default_params_reference_quirk(qglib):
+    import qgamd._lib as L
+    p = L.QgParams()
+    qglib.qg_default_params(C.byref(p))
+    # P_matrix(H_1, H_1) as evolve_psi! builds it (model.jl:173)
+    assert list(p.P_fwd) == [1.0, -1.0, 1.0, 1.0]
+    assert p.solver == L.QG_SOLVER_SPECTRAL
+
+
+def test_params_struct_layout_matches_c(tmp_path):
+    import qgamd._lib as L
+    fields = [f for f, _ in L.QgParams._fields_]
+    src = ["#include <stdio.h>", "#include <stddef.h>", '#include "qg_mi355.h"', "int main(void){",
+           'printf("%zu\\n", sizeof(qg_params));']
+    src += [f'printf("%zu\\n", offsetof(qg_params, {f}));' for f in fields]
+    src += ["return 0;}"]
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(c), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True,
+                                           check=True).stdout.split()]
+    assert vals[0] == C.sizeof(L.QgParams)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(L.QgParams, f).offset == off, f
+
+
+def test_create_rejects_bad_params_without_gpu(qglib):
+    import qgamd._lib as L
+    p = L.QgParams()
+    qglib.qg_default_params(C.byref(p))
+    ctx = C.c_void_p()
+    # M = 0 is rejected before any device work
+    assert qglib.qg_create(C.byref(p), 0, None, C.byref(ctx)) == -1

@@ -1,0 +1,209 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the golden
+fixtures.  Tolerances:
+  * stencils (laplace_5p, cd, J) and the seeded initial conditions: bit-exact (the stencil
+    file is compiled without FMA contraction and follows the reference evaluation order);
+  * solves and multi-step trajectories: relative RMS (2-norm) error < 1e-10 (north star),
+    measured values are ~1e-13.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def qg(torch):
+    import qgamd
+    qgamd.lib()
+    return qgamd
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import qg_oracle
+    qg_oracle.build()
+    return qg_oracle
+
+
+@pytest.fixture(scope="module")
+def R():
+    from oracle import qg_ref
+    return qg_ref
+
+
+def dev(torch, a):
+    """Julia-layout numpy (M+2, P+2) -> device tensor (P+2, M+2)."""
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float64).T)).cuda()
+
+
+def host(t):
+    return t.cpu().numpy().T
+
+
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+def rand_field(R, M, P, seed):
+    return R.update_doubly_periodic_bc(R.seeded_rand(M, P, seed) - 0.5)
+
+
+@pytest.mark.parametrize("M,P", [(8, 8), (16, 12), (33, 17), (128, 64), (300, 7)])
+def test_stencils_bitwise(torch, qg, R, M, P):
+    dx = 4e6 / M
+    z, p = rand_field(R, M, P, 11), rand_field(R, M, P, 12)
+    dz, dp = dev(torch, z), dev(torch, p)
+    assert np.array_equal(host(qg.laplace_5p(dp, dx)), R.laplace_5p(p, dx))
+    assert np.array_equal(host(qg.cd(dp, dx)), R.cd(p, dx))
+    assert np.array_equal(host(qg.J(dx, dz, dp)), R.J(dx, z, p))
+    b = R.seeded_rand(M, P, 3)
+    db = dev(torch, b)
+    qg.update_doubly_periodic_bc_(db)
+    assert np.array_equal(host(db), R.update_doubly_periodic_bc(b.copy()))
+
+
+@pytest.mark.parametrize("M,P", [(8, 8), (16, 16), (32, 24), (64, 100), (256, 64)])
+def test_helmholtz_solve_matches_direct(torch, qg, R, O, M, P):
+    dx = 4e6 / M
+    alpha = -6.25e-10
+    f = rand_field(R, M, P, 5) * 1e-9
+    got = host(qg.sp_solve_modified_helmholtz(M, P, dx, dev(torch, f), alpha))
+    ref = R.sp_solve_modified_helmholtz(M, P, dx, f, alpha) if M * P <= 65536 else \
+        O.solve(M, P, dx, alpha, f)
+    assert rel(got, ref) < 1e-12
+
+
+@pytest.mark.parametrize("M,P", [(8, 8), (16, 16), (32, 48), (128, 128)])
+def test_pinned_poisson_matches_direct(torch, qg, R, M, P):
+    dx = 4e6 / M
+    f = rand_field(R, M, P, 6) * 1e-9  # nonzero mean: exercises the compatibility shift
+    got = host(qg.sp_solve_poisson(M, P, dx, dev(torch, f)))
+    ref = R.sp_solve_poisson(M, P, dx, f)
+    assert rel(got, ref) < 1e-12
+    assert abs(got[1, 1]) <= 1e-13 * np.abs(ref).max()
+
+
+def test_helmholtz_manufactured_convergence(torch, qg, R):
+    """test.jl:150-193 on the device solver: same errors as the oracle, slope window."""
+    x0, x1 = 0, 3
+    Lx = x1 - x0
+    alpha = -3.0
+    u = lambda x, y: np.sin(2 * np.pi * x / Lx) * np.cos(2 * np.pi * y / Lx)
+    f = lambda x, y: -(np.pi ** 2) * (u(x, y) * (4 / Lx ** 2 + 4 / Lx ** 2)) + alpha * u(x, y)
+    errs = []
+    for M in [8, 16, 32, 64, 128, 256, 512]:
+        dx = Lx / M
+        xs = R.julia_range(x0 - dx, x1, M + 2)
+        b = R.inflate(f, xs, xs)
+        un = host(qg.sp_solve_modified_helmholtz(M, M, dx, dev(torch, b), alpha))
+        errs.append(dx * np.linalg.norm(un - R.inflate(u, xs, xs)))
+    slope = np.polyfit(np.log([8, 16, 32, 64, 128, 256, 512]), np.log(errs), 1)[0]
+    assert round(slope, 4) == -2.0495  # scheme_validation.ipynb
+
+
+def test_initial_conditions_bitwise(torch, qg, R):
+    m = qg.bench_model(32, P=24)
+    st = qg.initialise_model(m)
+    torch.cuda.synchronize()
+    z, p = R.initialise_model(R.bench_model(32, P=24))
+    assert np.array_equal(st.to_numpy("zeta"), z)
+    assert np.array_equal(st.to_numpy("psi"), p)
+    assert np.all(st.to_numpy("f_store") == 0)
+
+
+def test_golden_32x32_full_state_every_slot(torch, qg):
+    g = np.load(os.path.join(GOLDEN, "qg_32x32.npz"))
+    st = qg.initialise_model(qg.bench_model(32))
+    done = 0
+    for t in (1, 2, 3, 10):
+        st.run(done + 1, t - done)
+        done = t
+        for name in ("psi", "zeta", "f_store"):
+            assert rel(st.to_numpy(name), g[f"{name}_{t}"]) < TOL, (name, t)
+
+
+def test_golden_rectangular(torch, qg):
+    g = np.load(os.path.join(GOLDEN, "qg_64x32.npz"))
+    st = qg.run_model_no_output(qg.bench_model(64, P=32), nsteps=6)
+    assert rel(st.to_numpy("psi"), g["psi_6"]) < TOL
+    assert rel(st.to_numpy("zeta"), g["zeta_6"]) < TOL
+
+
+def test_golden_config1_128_one_day(torch, qg):
+    """BASELINE.json config 1 (128x128, dt = 30 min, T = 1 day) through run_model_no_output."""
+    g = np.load(os.path.join(GOLDEN, "qg_128x128_T1day.npz"))
+    st = qg.run_model_no_output(qg.bench_model(128))
+    psi, zeta = st.to_numpy("psi")[:, :, :, 0], st.to_numpy("zeta")[:, :, :, 0]
+    assert rel(psi, g["psi_48"]) < TOL
+    assert rel(zeta, g["zeta_48"]) < TOL
+
+
+def test_evolve_functions_match_step(torch, qg):
+    """evolve_zeta!/evolve_psi! called separately == qg_step; canonicalize restores order."""
+    m = qg.bench_model(64)
+    a = qg.initialise_model(m)
+    b = qg.initialise_model(m)
+    pc = qg.get_poisson_cholesky(m.M, m.P, m.dx)
+    hc = qg.get_helmholtz_cholesky(m.M, m.P, m.dx, qg.S_eig(m))
+    for t in range(1, 6):
+        qg.evolve_zeta_(m, a, t)
+        qg.evolve_psi_(m, a, pc, hc)
+        b.step(t)
+    for name in ("zeta", "psi", "f_store"):
+        assert np.array_equal(a.to_numpy(name), b.to_numpy(name))
+    before = a.to_numpy("psi")
+    a.canonicalize()
+    assert a.heads() == [0, 0, 0]
+    assert np.array_equal(a.to_numpy("psi"), before)
+    assert np.array_equal(a.psi.permute(3, 2, 1, 0).cpu().numpy(), before)
+
+
+@pytest.mark.parametrize("N,steps", [(128, 100), (256, 20)])
+def test_long_run_against_c_oracle(torch, qg, O, R, N, steps):
+    m = qg.bench_model(N)
+    st = qg.run_model_no_output(m, nsteps=steps)
+    ref = O.State(R.bench_model(N)).run(steps)
+    assert rel(st.to_numpy("psi"), ref.psi) < TOL
+    assert rel(st.to_numpy("zeta"), ref.zeta) < TOL
+
+
+@pytest.mark.slow
+def test_config2_1024_ten_steps(torch, qg, O, R):
+    """BASELINE.json config 2 size (1024x1024 F64): 10 steps vs the C oracle."""
+    N, steps = 1024, 10
+    st = qg.run_model_no_output(qg.bench_model(N), nsteps=steps)
+    ref = O.State(R.bench_model(N)).run(steps)
+    e = rel(st.to_numpy("psi")[:, :, :, 0], ref.psi[:, :, :, 0])
+    assert e < TOL, e
+
+
+def test_full_size_invariants_4096(torch, qg):
+    """At the 4096^2 bench size: the step conserves sum(zeta) to roundoff (Arakawa + periodic
+    operators are conservative), the Poisson mode stays pinned, nothing blows up."""
+    m = qg.bench_model(4096, dt=60.0)
+    st = qg.initialise_model(m)
+    z0 = float(st.current("zeta", 1).double()[1:-1, 1:-1].sum())
+    st.run(1, 4)
+    torch.cuda.synchronize()
+    psi1 = st.current("psi", 1)
+    assert torch.isfinite(psi1).all()
+    z1 = st.current("zeta", 1)[1:-1, 1:-1]
+    scale = float(z1.abs().max()) * z1.numel()
+    assert abs(float(z1.sum()) - z0) < 1e-12 * scale
+    # psi~_1 = (psi_1 + psi_2)/2 with P = [[1,-1],[1,1]]; pinned to 0 at interior (1,1)
+    p1, p2 = st.current("psi", 1), st.current("psi", 2)
+    pt1 = 0.5 * (float(p1[1, 1]) + float(p2[1, 1]))
+    assert abs(pt1) < 1e-12 * float(p1.abs().max())
