@@ -1,0 +1,203 @@
+"""Benchmark: timesteps/s of the 2-layer Phillips hot path (evolve_zeta! + evolve_psi!) on
+MI355X, with the HBM roofline of the dominant kernel and the CPU oracle timed beside it.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--dt 60]
+
+Workload (BASELINE.json configs[2]; per GPU for N > 1, slabs in y, weak scaling):
+  2-layer Phillips, N x N interior per GPU, Float64, bench parameters of
+  src/benchmarking/julia_bench_parts.jl:6-18 (H1 = 1 km, H2 = 2 km, beta = 2e-11,
+  Lx = 4000 km per GPU, U = 0.1, nu = 100, r = 1e-7, R_d = 40 km, kick = 1e-6) with a stable
+  dt = 60 s, seeded synthetic initial conditions.  A "step" is one timestep of the model:
+  the fused tendency + AB3 kernel, then the Poisson + Helmholtz inversion.  The timed steps
+  are AB3 steps (the two Euler steps are inside the warm-up when W >= 2).
+
+Output: one JSON line (rank 0).  `value` is whole-job throughput = (GPUs x steps) / time,
+i.e. N x N-slab timesteps per second summed over GPUs (a single GPU: model timesteps/s).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "julia-ocean-modelling_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "model timesteps/sec at N×N per GPU; achieved HBM GB/s vs roofline, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+B = 8  # bytes per double
+
+# algorithmic HBM bytes per interior grid point (both layers / both systems), see DESIGN.md
+BYTES_TENDENCY_AB3 = 2 * 6 * B  # per layer: read zeta, psi, F(t-1), F(t-2); write zeta+, F
+BYTES_SOLVE = 4 * 2 * B         # pass A: read zeta1,2 write u(2); pass B: read u(2) write psi1,2
+BYTES_STEP = BYTES_TENDENCY_AB3 + BYTES_SOLVE
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--n", type=int, default=4096, help="grid points per side per GPU")
+    ap.add_argument("--dt", type=float, default=60.0)
+    ap.add_argument("--chunk-rows", type=int, default=0)
+    ap.add_argument("--cpu-steps", type=int, default=3, help="CPU-oracle sample steps (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all threads OpenMP offers")
+    return ap.parse_args()
+
+
+def cpu_baseline(n, dt, steps, threads):
+    """Time the C oracle (oracle/qg_oracle.c, OpenMP) on a bounded sample of the same
+    workload: `steps` AB3 timesteps of the same n x n F64 model after its 2 Euler steps."""
+    from oracle import qg_oracle, qg_ref
+
+    qg_oracle.build()
+    m = qg_ref.bench_model(n, dt=dt)
+    st = qg_oracle.State(m, nthreads=threads)
+    st.run(2)  # the Euler steps (untimed)
+    t0 = time.perf_counter()
+    st.run(steps)
+    el = time.perf_counter() - t0
+    used = threads if threads > 0 else qg_oracle.lib().qgo_max_threads()
+    return {"value": steps / el, "unit": "timesteps/s", "cores": int(used), "kind": "port",
+            "sample": f"{steps} AB3 timesteps of the {n}x{n} F64 model (after its 2 Euler steps), "
+                      f"C oracle (exact DFT solve), {el:.2f} s wall"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import qgamd
+
+    n = args.n
+    m = qgamd.bench_model(n, dt=args.dt, P=n * world)
+    st = qgamd.State(m, chunk_rows=args.chunk_rows, P_local=n)
+    if world > 1:
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            import ctypes as C
+            buf = C.create_string_buffer(128)
+            qgamd._lib.call("qg_comm_unique_id", buf)
+            uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        st.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
+    st.initialise()
+
+    t = 1
+    for _ in range(args.warmup):
+        st.step(t)
+        t += 1
+    torch.cuda.synchronize()
+
+    K = args.steps
+    stream = torch.cuda.current_stream()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(K):
+        ev[k][0].record(stream)
+        st.evolve_zeta_(t)
+        ev[k][1].record(stream)
+        st.evolve_psi_()
+        ev[k][2].record(stream)
+        t += 1
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    tend_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / K
+    solve_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / K
+    finite = bool(torch.isfinite(st.current("psi", 1)).all().item())
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    pts = n * n
+    ms = el * 1e3 / K
+    tend_gbs = BYTES_TENDENCY_AB3 * pts / (tend_ms * 1e-3) / 1e9
+    step_gbs = BYTES_STEP * pts / (ms * 1e-3) / 1e9
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_tendency.json")
+    if os.path.exists(prof):
+        try:
+            pj = json.load(open(prof))
+            if pj.get("n") == n:
+                traffic = pj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    out = {
+        "metric": METRIC,
+        "value": world * K / el,
+        "unit": f"timesteps/s ({n}x{n} F64 slab-steps summed over GPUs)",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: seeded counter-based noise initial conditions (model.jl:41-42 uses unseeded rand)",
+        "config": {
+            "workload": f"2-layer Phillips {n}x{n} Float64 per GPU (BASELINE configs[2]), Arakawa "
+                        "tendency + AB3, pinned Poisson + modified Helmholtz inversion, dt = "
+                        f"{args.dt:g} s, bench params of julia_bench_parts.jl:6-18",
+            "grid_per_gpu": [n, n],
+            "global_grid": [n, n * world],
+            "parallelism": f"y-slab x{world}" if world > 1 else "single GPU",
+            "solver": "spectral (x-DFT + parallel cyclic tridiagonal in y, direct)",
+            "finite": finite,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "tendency_kernel (fused Arakawa J + biharmonic + beta + AB3, both layers)",
+            "achieved": tend_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": tend_gbs / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "avg_launch_ms": tend_ms,
+            "algorithmic_bytes_per_launch": BYTES_TENDENCY_AB3 * pts,
+        },
+        "step_roofline": {
+            "achieved": step_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": step_gbs / HBM_PEAK_GBS,
+            "algorithmic_bytes_per_step": BYTES_STEP * pts, "solve_ms": solve_ms, "tendency_ms": tend_ms,
+        },
+    }
+    if args.cpu_steps > 0 and world == 1:
+        out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
