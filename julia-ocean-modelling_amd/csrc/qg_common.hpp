@@ -64,6 +64,27 @@ __device__ __forceinline__ void store_with_ghosts(double *out, int64_t ld, int64
     }
 }
 
+// Same as store_with_ghosts for a whole row j that the caller walks: `row` = out + (j+1)*ld
+// and the ghost-row target `grow` (row 0 when j == P-1, row P+1 when j == 0, else nullptr)
+// are wave-uniform, so every store is an SGPR base + 32-bit lane offset.
+__device__ __forceinline__ void store_row_with_ghosts(double *row, double *grow, int M, int i, double v) {
+    row[i + 1] = v;
+    if (i == M - 1) row[0] = v;
+    if (i == 0) row[M + 1] = v;
+    if (grow) {
+        grow[i + 1] = v;
+        if (i == M - 1) grow[0] = v;
+        if (i == 0) grow[M + 1] = v;
+    }
+}
+
+__device__ __forceinline__ double *ghost_row_target(double *out, int64_t ld, int64_t P, int64_t j, bool ghost_rows) {
+    if (!ghost_rows) return nullptr;
+    if (j == P - 1) return out;                                     // ghost row j = -1
+    if (j == 0) return out + static_cast<size_t>(P + 1) * ld;       // ghost row j = P
+    return nullptr;
+}
+
 // counter-based uniform in [0,1) shared with oracle/qg_ref.py and oracle/qg_oracle.c
 __host__ __device__ inline double u01(uint64_t seed, uint64_t k) {
     uint64_t x = seed + (k + 1) * 0x9E3779B97F4A7C15ULL;

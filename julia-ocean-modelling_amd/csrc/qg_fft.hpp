@@ -60,13 +60,21 @@ __device__ __forceinline__ void dftR(double2 (&v)[R]) {
     else dft8<INV>(v);
 }
 
-// radix of the next pass: 8 while the remaining length allows it and the pass still gives
-// every thread a butterfly, else 4, else 2
+// radix of the next pass: 8 while the remaining length allows it and every thread still gets
+// a butterfly (or radix 4 would not fill the threads either), else 4, else 2
 template <int N, int T, int NS>
 struct PassRadix {
     static constexpr int REM = N / NS;
     static constexpr int value =
         (REM % 8 == 0 && (N / 8 >= T || N / 4 < T)) ? 8 : ((REM % 4 == 0) ? 4 : 2);
+};
+
+// LDS index with one pad slot per 8 complex values: keeps the radix-8 scatter of the first
+// pass (lane stride 8 x 16 B) free of ds_write_b128 bank conflicts.
+__host__ __device__ constexpr int lpad(int x) { return x + (x >> 3); }
+template <int N>
+struct LdsSize {
+    static constexpr int value = lpad(N - 1) + 1;  // complex elements
 };
 
 template <int N, int T, int R, int NS, bool INV>
@@ -81,13 +89,16 @@ __device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__res
         if (NB % T == 0 || j < NB) {
             const int k = j % NS;
 #pragma unroll
-            for (int r = 0; r < R; ++r) v[p][r] = buf[j + r * NB];
+            for (int r = 0; r < R; ++r) v[p][r] = buf[lpad(j + r * NB)];
             if constexpr (NS > 1) {
+                // W^(r k) by repeated multiplication of one table twiddle W^k (error <= R eps)
+                double2 w = tw[k * (N / (NS * R))];
+                if (INV) w.y = -w.y;
+                double2 wr = w;
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
-                    double2 w = tw[(r * k) * (N / (NS * R))];
-                    if (INV) w.y = -w.y;
-                    v[p][r] = cmul(v[p][r], w);
+                    v[p][r] = cmul(v[p][r], wr);
+                    if (r + 1 < R) wr = cmul(wr, w);
                 }
             }
             dftR<R, INV>(v[p]);
@@ -101,7 +112,7 @@ __device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__res
             const int k = j % NS;
             const int base = (j / NS) * NS * R + k;
 #pragma unroll
-            for (int r = 0; r < R; ++r) buf[base + r * NS] = v[p][r];
+            for (int r = 0; r < R; ++r) buf[lpad(base + r * NS)] = v[p][r];
         }
     }
     __syncthreads();
@@ -116,7 +127,7 @@ __device__ __forceinline__ void fft_passes(double2 *buf, const double2 *__restri
     }
 }
 
-// Unnormalised DFT of buf[0..N) in place (natural order in and out).  Caller must have
+// Unnormalised DFT of buf[lpad(0..N)) in place (natural order in and out).  Caller must have
 // synchronised after writing buf; returns after a barrier.
 template <int N, int T, bool INV>
 __device__ __forceinline__ void fft_lds(double2 *buf, const double2 *__restrict__ tw) {

@@ -13,10 +13,15 @@ constexpr int PIN_THREADS = 1024;
 
 template <int N>
 struct Geo {
-    static constexpr int T = N / 8 < 64 ? 64 : (N / 8 > 512 ? 512 : N / 8);  // threads per row
+    static constexpr int T = N / 4 < 64 ? 64 : (N / 4 > 1024 ? 1024 : N / 4);  // threads per row
+    // one workgroup of T threads per CU (72 KB of LDS at N = 4096): registers capped at
+    // 512 / (T / 256) per lane so the whole workgroup stays resident
+    static constexpr int MINW = T / 256 < 1 ? 1 : T / 256;
     static constexpr int KH = N / 2 + 1;
-    static constexpr int KQ = (KH + T - 1) / T;  // wavenumbers per thread
-    static constexpr int EP = (N + T - 1) / T;   // row elements per thread
+    // wavenumber slots per thread over k in [0, N/2); the real Nyquist line k = N/2 rides in
+    // the imaginary part of the (also real) k = 0 slot of thread 0
+    static constexpr int KQ = N / 2 >= T ? N / 2 / T : 1;
+    static constexpr int EP = (N + T - 1) / T;  // row elements per thread
 };
 
 __device__ __forceinline__ double2 cfma(double s, double2 x, double2 y) {  // s*x + y
@@ -27,27 +32,29 @@ __device__ __forceinline__ double2 cfma(double s, double2 x, double2 y) {  // s*
 // pass A: project + row DFT + chunk-local backward filter (one workgroup per chunk)
 // ------------------------------------------------------------------------------------
 template <int N>
-__global__ __launch_bounds__(Geo<N>::T) void spec_passA(SpecArgs a) {
+__global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a) {
     using G = Geo<N>;
-    constexpr int T = G::T, KH = G::KH, KQ = G::KQ, EP = G::EP;
+    constexpr int T = G::T, KQ = G::KQ, EP = G::EP, NH = N / 2;
     extern __shared__ double2 buf[];
     const int t = threadIdx.x, c = blockIdx.x;
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
     const int64_t ld = a.ld;
-    double2 u[KQ][2], wl[KQ][2];
-    double wg[KQ][2];
+    // u: backward filter state.  bw: WLS scaled by r^-(e-j) (bw_j = bw_{j+1} r^-1 + u_j, so
+    // WLS = bw_s r^(L-1) needs no running weight).  Slot (0, t = 0): .x = k 0, .y = k N/2.
+    double2 u[KQ][2], bw[KQ][2];
 #pragma unroll
     for (int q = 0; q < KQ; ++q)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             u[q][s] = make_double2(0, 0);
-            wl[q][s] = make_double2(0, 0);
-            wg[q][s] = 1.0;
+            bw[q][s] = make_double2(0, 0);
         }
+    const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
     double dc = 0;
     double *hline = a.rec + rec_HLINE(KS);
     for (int j = e; j >= s0; --j) {
+        asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
         const double *r1 = a.in1 + fidx(1, j + 1, ld);
         const double *r2 = a.in2 + fidx(1, j + 1, ld);
 #pragma unroll
@@ -55,7 +62,7 @@ __global__ __launch_bounds__(Geo<N>::T) void spec_passA(SpecArgs a) {
             const int i = t + p * T;
             if (N % T == 0 || i < N) {
                 const double x1 = r1[i], x2 = r2[i];
-                buf[i] = make_double2(a.pin_in[0] * x1 + a.pin_in[1] * x2, a.pin_in[2] * x1 + a.pin_in[3] * x2);
+                buf[lpad(i)] = make_double2(p0 * x1 + p1 * x2, p2 * x1 + p3 * x2);
             }
         }
         __syncthreads();
@@ -64,22 +71,32 @@ __global__ __launch_bounds__(Geo<N>::T) void spec_passA(SpecArgs a) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
-            if (KH % T == 0 || k < KH) {
-                const double2 Zk = buf[k], Zm = buf[(N - k) & (N - 1)];
-                double2 B[2];
-                B[0] = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
-                B[1] = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
-                if (k == 0) {
-                    dc += B[0].x;
-                    hline[j] = B[0].x;
-                }
+            if (NH % T == 0 || k < NH) {
+                const double2 Zk = buf[lpad(k)];
+                if (k == 0) {  // the two real lines k = 0 and k = N/2
+                    const double2 Zn = buf[lpad(NH)];
+                    dc += Zk.x;
+                    hline[j] = Zk.x;
+                    const double2 B[2] = {make_double2(Zk.x, Zn.x), make_double2(Zk.y, Zn.y)};
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const double r = a.coef[s * KS + k].r;
-                    u[q][s] = cfma(r, u[q][s], B[s]);
-                    Urow[s * KS + k] = u[q][s];
-                    wl[q][s] = cfma(wg[q][s], u[q][s], wl[q][s]);
-                    wg[q][s] *= r;
+                    for (int s = 0; s < 2; ++s) {
+                        const Coef *c0 = a.coef + s * KS, *cN = a.coef + s * KS + NH;
+                        u[q][s] = make_double2(c0->cs * B[s].x + c0->r * u[q][s].x, cN->cs * B[s].y + cN->r * u[q][s].y);
+                        Urow[s * KS] = make_double2(u[q][s].x, 0);
+                        Urow[s * KS + NH] = make_double2(u[q][s].y, 0);
+                        bw[q][s] = make_double2(bw[q][s].x * c0->rinv + u[q][s].x, bw[q][s].y * cN->rinv + u[q][s].y);
+                    }
+                } else {
+                    const double2 Zm = buf[lpad(N - k)];
+                    const double2 B[2] = {make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5),
+                                          make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5)};
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const Coef *cf = a.coef + s * KS + k;
+                        u[q][s] = cfma(cf->r, u[q][s], cscale(B[s], cf->cs));
+                        Urow[s * KS + k] = u[q][s];
+                        bw[q][s] = cfma(cf->rinv, bw[q][s], u[q][s]);
+                    }
                 }
             }
         }
@@ -88,11 +105,20 @@ __global__ __launch_bounds__(Geo<N>::T) void spec_passA(SpecArgs a) {
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
         const int k = t + q * T;
-        if (KH % T == 0 || k < KH) {
+        if (NH % T == 0 || k < NH) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                a.ULS[((size_t)c * 2 + s) * KS + k] = u[q][s];
-                a.WLS[((size_t)c * 2 + s) * KS + k] = wl[q][s];
+                const size_t o = ((size_t)c * 2 + s) * KS;
+                if (k == 0) {
+                    const double q0 = a.coef[s * KS].qm1, qN = a.coef[s * KS + NH].qm1;
+                    a.ULS[o] = make_double2(u[q][s].x, 0);
+                    a.ULS[o + NH] = make_double2(u[q][s].y, 0);
+                    a.WLS[o] = make_double2(bw[q][s].x * q0, 0);
+                    a.WLS[o + NH] = make_double2(bw[q][s].y * qN, 0);
+                } else {
+                    a.ULS[o + k] = u[q][s];
+                    a.WLS[o + k] = cscale(bw[q][s], a.coef[s * KS + k].qm1);
+                }
             }
         }
     }
@@ -238,12 +264,12 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
         const double rPl1 = exp((double)(Pl - 1) * cf.lr);
         auto AU = [&](int g) {
             double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AU(KS))[s * KS + k];
-            if (dl && g == 0) v.x += delta;
+            if (dl && g == 0) v.x += cf.cs * delta;
             return v;
         };
         auto AW = [&](int g) {
             double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AW(KS))[s * KS + k];
-            if (dl && g == 0) v.x += rPl1 * delta;
+            if (dl && g == 0) v.x += rPl1 * (cf.cs * delta);
             return v;
         };
         auto Uext = [&](int g) {  // u_true at the start of rank g+1 (ring)
@@ -266,11 +292,11 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
             const double2 ue0 = a.rank == 0 ? ue : Uext(0);
             const double2 we0 = a.rank == 0 ? we : Wext(0);
             double2 u0 = reinterpret_cast<const double2 *>(rec(0) + rec_ULS0(KS))[k];
-            u0.x += delta;
+            u0.x += cf.cs * delta;
             const double2 uin0 = cfma(exp((double)(a.Nc - 1) * a.L * cf.lr), ue0,
                                       reinterpret_cast<const double2 *>(rec(0) + rec_UIN0(KS))[k]);
             const double2 w0 = cfma(cf.r, we0, cfma(cf.q, uin0, u0));
-            const double X = cf.cs * w0.x;
+            const double X = w0.x;
             pin_part += (2 * k == a.M) ? X : 2 * X;
         }
     }
@@ -315,10 +341,26 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
 // ------------------------------------------------------------------------------------
 // pass B: forward filter with carries, inverse row DFT, pin, back-projection, store
 // ------------------------------------------------------------------------------------
+// carry-in state of line (s, k) entering chunk c: cu = r^L u_in, w = w_in (see header)
+__device__ __forceinline__ void chunk_carry(const SpecArgs &a, int s, int k, int c, double delta, bool inject,
+                                            double2 &cu, double2 &w) {
+    const Coef cf = a.coef[s * a.KS + k];
+    const double2 Ue = a.EXT[(size_t)s * a.KS + k], We = a.EXT[(size_t)(2 + s) * a.KS + k];
+    const int64_t n = (int64_t)c * a.L;
+    const double2 uin = cfma(exp((double)(a.Nc - 1 - c) * a.L * cf.lr), Ue, a.UIN[((size_t)c * 2 + s) * a.KS + k]);
+    cu = cscale(uin, cf.q);
+    double gc = 0;
+    if (n > 0) gc = exp((double)(a.P - n + 1) * cf.lr) * (expm1(2.0 * n * cf.lr) / expm1(2.0 * cf.lr));
+    double2 wi = cfma(gc, Ue, a.WIN[((size_t)c * 2 + s) * a.KS + k]);
+    wi = cfma(exp((double)n * cf.lr), We, wi);
+    if (s == 0 && inject && c >= 1) wi.x += exp((double)(n - 1) * cf.lr) * (cf.cs * delta);
+    w = wi;
+}
+
 template <int N>
-__global__ __launch_bounds__(Geo<N>::T) void spec_passB(SpecArgs a) {
+__global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a) {
     using G = Geo<N>;
-    constexpr int T = G::T, KH = G::KH, KQ = G::KQ, EP = G::EP;
+    constexpr int T = G::T, KQ = G::KQ, EP = G::EP, NH = N / 2;
     extern __shared__ double2 buf[];
     const int t = threadIdx.x, c = blockIdx.x;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
@@ -326,72 +368,89 @@ __global__ __launch_bounds__(Geo<N>::T) void spec_passB(SpecArgs a) {
     const int64_t Pl = a.P, ld = a.ld;
     const double delta = a.scal[0], pin = a.scal[1];
     const bool inject = a.pinned0 && a.rank == 0;
+    const bool sing = a.pinned0;  // (s = 0, k = 0) is the singular line, served by a.line
 
-    double2 uin[KQ][2], w[KQ][2];
-    double pw[KQ][2];
+    // per line: carried term cu = r^(e+1-j) u_in and forward-filter state w.  Slot (0, t = 0)
+    // packs the real lines k = 0 (.x) and k = N/2 (.y).
+    double2 cu[KQ][2], w[KQ][2];
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
         const int k = t + q * T;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
-            uin[q][s] = make_double2(0, 0);
+            cu[q][s] = make_double2(0, 0);
             w[q][s] = make_double2(0, 0);
-            pw[q][s] = 0;
-            if ((KH % T == 0 || k < KH) && !(s == 0 && a.pinned0 && k == 0)) {
-                const Coef cf = a.coef[s * KS + k];
-                const double2 Ue = a.EXT[(size_t)s * KS + k], We = a.EXT[(size_t)(2 + s) * KS + k];
-                const int64_t n = (int64_t)c * L;
-                uin[q][s] = cfma(exp((double)(a.Nc - 1 - c) * L * cf.lr), Ue, a.UIN[((size_t)c * 2 + s) * KS + k]);
-                double gc = 0;
-                if (n > 0) gc = exp((double)(Pl - n + 1) * cf.lr) * (expm1(2.0 * n * cf.lr) / expm1(2.0 * cf.lr));
-                double2 wi = cfma(gc, Ue, a.WIN[((size_t)c * 2 + s) * KS + k]);
-                wi = cfma(exp((double)n * cf.lr), We, wi);
-                if (s == 0 && inject && c >= 1) wi.x += exp((double)(n - 1) * cf.lr) * delta;
-                w[q][s] = wi;
-                pw[q][s] = cf.q;
+            if (NH % T == 0 || k < NH) {
+                if (k == 0) {
+                    double2 c0 = make_double2(0, 0), w0 = make_double2(0, 0), cN, wN;
+                    if (!(s == 0 && sing)) chunk_carry(a, s, 0, c, delta, inject, c0, w0);
+                    chunk_carry(a, s, NH, c, delta, inject, cN, wN);
+                    cu[q][s] = make_double2(c0.x, cN.x);
+                    w[q][s] = make_double2(w0.x, wN.x);
+                } else {
+                    chunk_carry(a, s, k, c, delta, inject, cu[q][s], w[q][s]);
+                }
             }
         }
     }
-
     for (int j = s0; j <= e; ++j) {
-        const double2 *Urow = a.U + (size_t)j * 2 * KS;
+        // compiler memory barrier: re-read the (L1-resident) coefficients every row instead of
+        // hoisting them into registers, which would spill at this occupancy
+        asm volatile("" ::: "memory");
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
-            if (KH % T == 0 || k < KH) {
+            if (NH % T == 0 || k < NH) {
+                const double2 *Urow = a.U + (size_t)j * 2 * KS;
                 double2 X[2];
+                if (k == 0) {
+                    double x0[2], xN[2];
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    if (s == 0 && a.pinned0 && k == 0) {
-                        X[s] = make_double2(a.line[j], 0);
-                    } else {
+                    for (int s = 0; s < 2; ++s) {
+                        const Coef *c0 = a.coef + s * KS, *cN = a.coef + s * KS + NH;
+                        double ul0 = Urow[s * KS].x, ulN = Urow[s * KS + NH].x;
+                        if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
+                            ul0 += c0->cs * delta;
+                            ulN += cN->cs * delta;
+                        }
+                        const double wx = c0->r * w[q][s].x + (ul0 + cu[q][s].x);
+                        const double wy = cN->r * w[q][s].y + (ulN + cu[q][s].y);
+                        w[q][s] = make_double2(wx, wy);
+                        cu[q][s] = make_double2(cu[q][s].x * c0->rinv, cu[q][s].y * cN->rinv);
+                        x0[s] = (s == 0 && sing) ? a.line[j] : wx;
+                        xN[s] = wy;
+                    }
+                    buf[lpad(0)] = make_double2(x0[0], x0[1]);
+                    buf[lpad(NH)] = make_double2(xN[0], xN[1]);
+                } else {
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
                         const Coef *cf = a.coef + s * KS + k;
                         double2 ul = Urow[s * KS + k];
-                        if (s == 0 && inject && j == 0) ul.x += delta;
-                        const double2 ut = cfma(pw[q][s], uin[q][s], ul);
-                        w[q][s] = cfma(cf->r, w[q][s], ut);
-                        pw[q][s] *= cf->rinv;
-                        X[s] = cscale(w[q][s], cf->cs);
+                        if (s == 0 && inject && j == 0) ul.x += cf->cs * delta;
+                        w[q][s] = cfma(cf->r, w[q][s], cadd(ul, cu[q][s]));
+                        cu[q][s] = cscale(cu[q][s], cf->rinv);
+                        X[s] = w[q][s];
                     }
+                    buf[lpad(k)] = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
+                    buf[lpad(N - k)] = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
                 }
-                buf[k] = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
-                if (k != 0 && 2 * k != N) buf[N - k] = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
             }
         }
         __syncthreads();
         fft_lds<N, T, true>(buf, a.tw);
+        double *row1 = a.out1 + (size_t)(j + 1) * ld;
+        double *grow1 = ghost_row_target(a.out1, ld, Pl, j, a.write_ghost_rows);
+        double *row2 = a.out2 ? a.out2 + (size_t)(j + 1) * ld : nullptr;
+        double *grow2 = a.out2 ? ghost_row_target(a.out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
 #pragma unroll
         for (int p = 0; p < EP; ++p) {
             const int i = t + p * T;
             if (N % T == 0 || i < N) {
-                const double2 z = buf[i];
+                const double2 z = buf[lpad(i)];
                 const double x1 = z.x - pin, x2 = z.y;
-                const double o1 = a.pin_out[0] * x1 + a.pin_out[1] * x2;
-                store_with_ghosts(a.out1, ld, N, Pl, i, j, o1, a.write_ghost_rows);
-                if (a.out2) {
-                    const double o2 = a.pin_out[2] * x1 + a.pin_out[3] * x2;
-                    store_with_ghosts(a.out2, ld, N, Pl, i, j, o2, a.write_ghost_rows);
-                }
+                store_row_with_ghosts(row1, grow1, N, i, a.pin_out[0] * x1 + a.pin_out[1] * x2);
+                if (row2) store_row_with_ghosts(row2, grow2, N, i, a.pin_out[2] * x1 + a.pin_out[3] * x2);
             }
         }
         __syncthreads();
@@ -403,7 +462,7 @@ __global__ __launch_bounds__(Geo<N>::T) void spec_passB(SpecArgs a) {
 // ------------------------------------------------------------------------------------
 template <int N>
 static int launch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
-    const size_t lds = sizeof(double2) * N;
+    const size_t lds = sizeof(double2) * LdsSize<N>::value;
     if (passB) {
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         spec_passB<N><<<a.Nc, Geo<N>::T, lds, s>>>(a);
@@ -494,6 +553,8 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
             cf.rinv = (double)(1 / r);
             cf.lr = (double)lr;
             cf.q = (double)expl(L * lr);
+            cf.qm1 = (double)expl((L - 1) * lr);
+            if (-(L - 1) * lr > 600) return QG_ERR_UNSUPPORTED;  // r^-(L-1) scaling would overflow
             cf.gam = (double)(r * expm1l(2 * L * lr) / expm1l(2 * lr));
             cf.rP = (double)expl((long double)P * lr);
             cf.gamP = (double)(r * expm1l(2 * (long double)P * lr) / expm1l(2 * lr));

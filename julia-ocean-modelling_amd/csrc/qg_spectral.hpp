@@ -6,18 +6,18 @@
 //   1. pass A   one workgroup per chunk of L rows.  Each row of the two right-hand sides is
 //               projected, packed as z = f1 + i f2, DFT'd in LDS, split into the two
 //               half-spectra; every wavenumber k then runs the backward first-order filter
-//               u_j = F_j + r_k u_{j+1} of the cyclic tridiagonal line solve
-//               X_{j-1} - 2 rho_k X_j + X_{j+1} = dx^2 F_j (factored as (1-rS)(1-rS^-1)),
-//               chunk-local (zero carry).  Writes u (the only full-size intermediate) and two
-//               complex chunk summaries per (system, k).
+//               u_j = cs_k F_j + r_k u_{j+1} of the cyclic tridiagonal line solve
+//               X_{j-1} - 2 rho_k X_j + X_{j+1} = dx^2 F_j (factored as (1-rS)(1-rS^-1); the
+//               output scale cs_k = -r_k dx^2 / M is applied up front, everything after is
+//               linear), chunk-local (zero carry).  Writes u (the only full-size
+//               intermediate) and two complex chunk summaries per (system, k).
 //   2. carry    segment-parallel scans over chunks -> chunk carry-ins (local to this rank)
 //               and rank aggregates.
 //   3. [RCCL all-gather of the rank records when the y direction is split over GPUs]
 //   4. pin      one workgroup: cross-rank carries, Poisson compatibility shift delta, the
 //               singular k = 0 Poisson line (double prefix sum), the pinning value.
-//   5. pass B   one workgroup per chunk: forward filter w_j = u_true_j + r w_{j-1} with the
-//               carries, X = -r dx^2 w / M, inverse DFT in LDS, pin, back-projection, store
-//               with the ghost ring.
+//   5. pass B   one workgroup per chunk: forward filter X_j = u_true_j + r X_{j-1} with the
+//               carries, inverse DFT in LDS, pin, back-projection, store with the ghost ring.
 // HBM traffic per grid point for both systems: read 2 + write 2 (pass A), read 2 + write 2
 // (pass B) doubles, plus ~0.5 double of chunk summaries.
 #pragma once
@@ -26,8 +26,8 @@
 
 namespace qg {
 
-struct Coef {  // per (system, k); see SpectralSolver::build_tables
-    double r, rinv, lr, q, gam, rP, gamP, cs, inv1mrPt, pad;
+struct Coef {  // per (system, k); see SpectralSolver::init
+    double r, rinv, lr, q, gam, rP, gamP, cs, inv1mrPt, qm1;  // qm1 = r^(L-1)
 };
 
 struct SpecArgs {

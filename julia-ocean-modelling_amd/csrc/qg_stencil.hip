@@ -10,6 +10,8 @@
 //   eulers_method / AB3   src/model.jl:123-136
 //   ghost ring            src/schemes/boundary_conditions.jl:2-13
 //   initialise_model      src/model.jl:37-62
+#include <cstdlib>
+
 #include "qg_common.hpp"
 
 namespace qg {
@@ -84,25 +86,29 @@ __global__ void fill_ghosts_kernel(double *b, int64_t M, int64_t P, int rows_too
 
 // ------------------------------------------------------------------------------------
 // Fused tendency + Euler/AB3 update (evolve_zeta!, model.jl:155-170), one layer per
-// blockIdx.z.  Each block owns TX columns and marches down a strip of rows keeping rolling
-// LDS rings: psi (5 rows, x-halo 2), zeta (4 rows, x-halo 1), lap(psi) (3 rows, x-halo 1).
-// Every psi / zeta row is read from HBM once per strip (plus the strip's 4 / 2 halo rows).
-// Per interior point the kernel reads zeta, psi, [F(t-1), F(t-2)] and writes zeta+, F.
+// blockIdx.z.  Each block owns TX columns (one per thread) and marches down a strip of
+// rows.  Rolling LDS rings hold psi (6 rows, x-halo 2), zeta (5 rows, x-halo 1) and
+// lap(psi) (4 rows, x-halo 1); the ring depths let one barrier per row suffice.  Row j+3 of
+// psi, row j+2 of zeta and F(t-1), F(t-2) of row j+1 are fetched into registers while row
+// j is computed (software pipeline), so HBM latency hides behind the stencil arithmetic.
+// Per interior point: read zeta, psi, [F(t-1), F(t-2)], write zeta+, F (+ ghost images).
 // ------------------------------------------------------------------------------------
-template <int TX>
+template <int TX, int PF>
 __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_block) {
+    constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
     const int layer = blockIdx.z;
     const int t = threadIdx.x;
-    const int64_t M = a.M, P = a.P, ld = a.ld;
-    const int64_t x0 = (int64_t)blockIdx.x * TX;
-    const int64_t i = x0 + t;
+    const int M = (int)a.M, P = (int)a.P;
+    const int64_t ld = a.ld;
+    const int x0 = blockIdx.x * TX;
+    const int i = x0 + t;
     const int jb0 = a.j0 + blockIdx.y * rows_per_block;
     const int jb1 = min(jb0 + rows_per_block, a.j1);
     if (jb0 >= jb1) return;  // uniform over the block
 
-    __shared__ double sp[5][TX + 4];
-    __shared__ double sz[4][TX + 2];
-    __shared__ double sl[3][TX + 2];
+    __shared__ double sp[RP][TX + 4];
+    __shared__ double sz[RZ][TX + 2];
+    __shared__ double sl[RL][TX + 2];
 
     const double *psi = a.psi[layer];
     const double *zeta = a.zeta[layer];
@@ -111,54 +117,123 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
     const double idx = 1.0 / a.dx, idx2 = idx * idx;
     const double cdc = 0.5 * idx;
     const double den = 12 * (a.dx * a.dx);
-    const int Mi = (int)M;
+    const bool small = M < TX + 4;
 
+    auto wx = [&](int x) -> int {  // periodic wrap of an interior column index
+        if (small) return ((x % M) + M) % M;
+        return x < 0 ? x + M : (x >= M ? x - M : x);
+    };
     auto rowp = [&](const double *base, const RowSrc &rs, int j) -> const double * {
         if (j >= 0 && j < P) return base + fidx(1, j + 1, ld);
-        return rs.halo[j < 0 ? j + 2 : (int)(j - P) + 2];
+        return rs.halo[j < 0 ? j + 2 : (j - P) + 2];
     };
-    auto xw = [&](int64_t x) -> int64_t {
-        int xi = (int)(x % Mi);
-        return xi < 0 ? xi + Mi : xi;
-    };
-    auto load_psi = [&](int j) {
+    // per-thread column positions: psi LDS position t+2 (own) and the halo position
+    const int ph_q = t < 2 ? t : (t >= TX - 2 ? t + 4 : -1);   // psi halo slot or none
+    const int zh_q = t == 0 ? 0 : (t == TX - 1 ? TX + 1 : -1);  // zeta halo slot or none
+    const int xo = wx(i);
+    const int xph = ph_q >= 0 ? wx(x0 - 2 + ph_q) : 0;
+    const int xzh = zh_q >= 0 ? wx(x0 - 1 + zh_q) : 0;
+    const bool has_out = i < M;
+    const bool ab3 = a.ab3 != 0;
+
+    // prefetch pipeline PF rows deep: slot 0 is consumed next
+    double pc[PF], ph[PF], zc[PF], zh[PF], f1[PF], f2[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) pc[k] = ph[k] = zc[k] = zh[k] = f1[k] = f2[k] = 0;
+    auto fetch_psi = [&](int j, double &c, double &h) {
         const double *r = rowp(psi, prs, j);
-        double *dst = sp[(j + 10) % 5];
-        for (int q = t; q < TX + 4; q += TX) dst[q] = r[xw(x0 - 2 + q)];
+        c = r[xo];
+        if (ph_q >= 0) h = r[xph];
     };
-    auto load_zeta = [&](int j) {
+    auto fetch_zeta = [&](int j, double &c, double &h) {
         const double *r = rowp(zeta, zrs, j);
-        double *dst = sz[(j + 8) % 4];
-        for (int q = t; q < TX + 2; q += TX) dst[q] = r[xw(x0 - 1 + q)];
+        c = r[xo];
+        if (zh_q >= 0) h = r[xzh];
     };
-    auto lap_row = [&](int j) {  // lap(psi) at row j, positions x0-1 .. x0+TX
-        const double *pm = sp[(j - 1 + 10) % 5], *p0 = sp[(j + 10) % 5], *pp = sp[(j + 1 + 10) % 5];
-        double *dst = sl[(j + 3) % 3];
+    auto fetch_f = [&](int j, double &g1, double &g2) {
+        if (ab3 && has_out) {
+            const size_t o = (size_t)(j + 1) * ld;  // uniform row offset
+            g1 = (a.fprev1[layer] + o)[i + 1];
+            g2 = (a.fprev2[layer] + o)[i + 1];
+        }
+    };
+    auto commit_psi = [&](int j, double c, double h) {
+        double *d = sp[(j + 2 * RP) % RP];
+        d[t + 2] = c;
+        if (ph_q >= 0) d[ph_q] = h;
+    };
+    auto commit_zeta = [&](int j, double c, double h) {
+        double *d = sz[(j + 2 * RZ) % RZ];
+        d[t + 1] = c;
+        if (zh_q >= 0) d[zh_q] = h;
+    };
+    auto lap_row = [&](int j) {  // lap(psi) at row j, LDS positions 0..TX+1 (x0-1 .. x0+TX)
+        const double *pm = sp[(j - 1 + 2 * RP) % RP], *p0 = sp[(j + 2 * RP) % RP], *pp = sp[(j + 1 + 2 * RP) % RP];
+        double *dst = sl[(j + 2 * RL) % RL];
         for (int q = t; q < TX + 2; q += TX) {
             const int c = q + 1;
             dst[q] = ((((p0[c - 1] + p0[c + 1]) - 4 * p0[c]) + pm[c]) + pp[c]) * idx2;
         }
     };
 
-    // prologue: psi rows jb0-2..jb0+1, zeta rows jb0-1..jb0, lap rows jb0-1, jb0
-    for (int j = jb0 - 2; j <= jb0 + 1; ++j) load_psi(j);
-    load_zeta(jb0 - 1);
-    load_zeta(jb0);
+    // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 straight into LDS
+    for (int j = jb0 - 2; j <= jb0 + 2; ++j) {
+        double c = 0, h = 0;
+        fetch_psi(j, c, h);
+        commit_psi(j, c, h);
+    }
+    for (int j = jb0 - 1; j <= jb0 + 1; ++j) {
+        double c = 0, h = 0;
+        fetch_zeta(j, c, h);
+        commit_zeta(j, c, h);
+    }
+    // prefetch for iterations jb0 .. jb0+PF-1: psi row j+3, zeta row j+2 (committed while
+    // rows are still needed, i.e. j+2 <= jb1) and F of row j
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int j = jb0 + k;
+        if (j + 2 <= jb1) {
+            fetch_psi(j + 3, pc[k], ph[k]);
+            fetch_zeta(j + 2, zc[k], zh[k]);
+        }
+        if (j < jb1) fetch_f(j, f1[k], f2[k]);
+    }
     __syncthreads();
     lap_row(jb0 - 1);
     lap_row(jb0);
+    lap_row(jb0 + 1);
 
     const double bl = a.beta[layer];
     for (int j = jb0; j < jb1; ++j) {
-        load_psi(j + 2);
-        load_zeta(j + 1);
+        const bool more = j + 2 <= jb1;  // psi row j+3 / zeta row j+2 / lap row j+2 needed
+        if (more) {
+            commit_psi(j + 3, pc[0], ph[0]);
+            commit_zeta(j + 2, zc[0], zh[0]);
+        }
+        const double f1c = f1[0], f2c = f2[0];
+#pragma unroll
+        for (int k = 0; k + 1 < PF; ++k) {
+            pc[k] = pc[k + 1];
+            ph[k] = ph[k + 1];
+            zc[k] = zc[k + 1];
+            zh[k] = zh[k + 1];
+            f1[k] = f1[k + 1];
+            f2[k] = f2[k + 1];
+        }
+        {
+            const int jn = j + PF;  // iteration whose inputs are fetched now
+            if (jn + 2 <= jb1) {
+                fetch_psi(jn + 3, pc[PF - 1], ph[PF - 1]);
+                fetch_zeta(jn + 2, zc[PF - 1], zh[PF - 1]);
+            }
+            if (jn < jb1) fetch_f(jn, f1[PF - 1], f2[PF - 1]);
+        }
         __syncthreads();
-        lap_row(j + 1);
-        __syncthreads();
-        if (i < M) {
-            const double *Lm = sl[(j - 1 + 3) % 3], *L0 = sl[(j + 3) % 3], *Lp = sl[(j + 1 + 3) % 3];
-            const double *Pm = sp[(j - 1 + 10) % 5], *P0 = sp[(j + 10) % 5], *Pp = sp[(j + 1 + 10) % 5];
-            const double *Zm = sz[(j - 1 + 8) % 4], *Z0 = sz[(j + 8) % 4], *Zp = sz[(j + 1 + 8) % 4];
+        if (more) lap_row(j + 2);
+        if (has_out) {
+            const double *Lm = sl[(j - 1 + 2 * RL) % RL], *L0 = sl[(j + 2 * RL) % RL], *Lp = sl[(j + 1 + 2 * RL) % RL];
+            const double *Pm = sp[(j - 1 + 2 * RP) % RP], *P0 = sp[(j + 2 * RP) % RP], *Pp = sp[(j + 1 + 2 * RP) % RP];
+            const double *Zm = sz[(j - 1 + 2 * RZ) % RZ], *Z0 = sz[(j + 2 * RZ) % RZ], *Zp = sz[(j + 1 + 2 * RZ) % RZ];
             const int cl = t + 1;  // centre in sl / sz (x-halo 1)
             const int cp = t + 2;  // centre in sp (x-halo 2)
             const double biharm = ((((L0[cl - 1] + L0[cl + 1]) - 4 * L0[cl]) + Lm[cl]) + Lp[cl]) * idx2;
@@ -177,17 +252,13 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
             if (layer == 0) last = a.U * (cdc * (Z0[cl + 1] - Z0[cl - 1]));  // U * cd(zeta)
             else last = a.r * L0[cl];                                         // r * lap(psi)
             const double F = ((v_term - J_term) - beta_term) - last;
-            const double zc = Z0[cl];
-            double zn;
-            const size_t o = fidx(i + 1, j + 1, ld);
-            if (!a.ab3) {
-                zn = zc + (a.dt * F);
-            } else {
-                const double f2 = a.fprev1[layer][o], f3 = a.fprev2[layer][o];
-                zn = zc + a.dt * ((((23.0 / 12.0) * F) - ((16.0 / 12.0) * f2)) + ((5.0 / 12.0) * f3));
-            }
-            store_with_ghosts(a.zeta_out[layer], ld, M, P, i, j, zn, a.write_ghost_rows);
-            store_with_ghosts(a.f_out[layer], ld, M, P, i, j, F, a.write_ghost_rows);
+            const double zcen = Z0[cl];
+            const double zn = ab3 ? zcen + a.dt * ((((23.0 / 12.0) * F) - ((16.0 / 12.0) * f1c)) + ((5.0 / 12.0) * f2c))
+                                  : zcen + (a.dt * F);
+            double *zo = a.zeta_out[layer], *fo = a.f_out[layer];
+            const bool gr = a.write_ghost_rows;
+            store_row_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
+            store_row_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
         }
     }
 }
@@ -260,15 +331,37 @@ int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s) {
     return QG_OK;
 }
 
-int launch_tendency(const TendArgs &a, hipStream_t s) {
-    constexpr int TX = 128;
-    const int rows = 32;
+template <int TX, int PF>
+static int launch_tend_variant(const TendArgs &a, int rows, hipStream_t s) {
     const int nrows = a.j1 - a.j0;
-    if (nrows <= 0) return QG_OK;
     dim3 grid((unsigned)((a.M + TX - 1) / TX), (unsigned)((nrows + rows - 1) / rows), 2);
-    tendency_kernel<TX><<<grid, TX, 0, s>>>(a, rows);
+    tendency_kernel<TX, PF><<<grid, TX, 0, s>>>(a, rows);
     QG_LAUNCH_CHECK();
     return QG_OK;
+}
+
+// Tile/pipeline variant (tuning knob; default 0).  QG_TEND_VARIANT selects it at run time.
+static int tend_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = std::getenv("QG_TEND_VARIANT");
+        v = e ? std::atoi(e) : 0;
+    }
+    return v;
+}
+
+int launch_tendency(const TendArgs &a, hipStream_t s) {
+    if (a.j1 - a.j0 <= 0) return QG_OK;
+    switch (tend_variant()) {
+        case 1: return launch_tend_variant<256, 1>(a, 32, s);
+        case 2: return launch_tend_variant<128, 1>(a, 64, s);
+        case 3: return launch_tend_variant<256, 1>(a, 128, s);
+        case 4: return launch_tend_variant<256, 2>(a, 64, s);
+        case 5: return launch_tend_variant<512, 1>(a, 64, s);
+        case 6: return launch_tend_variant<128, 2>(a, 64, s);
+        case 7: return launch_tend_variant<256, 3>(a, 64, s);
+        default: return launch_tend_variant<256, 1>(a, 64, s);
+    }
 }
 
 // seeded initialise_model; P = local rows, P_total / j_offset place the slab in the global grid

@@ -1,0 +1,24 @@
+"""Time the tendency kernel (qg_evolve_zeta) and the solve at 4096^2 for the variant selected
+by QG_TEND_VARIANT (tuning helper, not part of the product)."""
+import json, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+import torch
+import qgamd
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+K = 20
+st = qgamd.State(qgamd.bench_model(n, dt=60.0)).initialise()
+for t in range(1, 6):
+    st.step(t)
+torch.cuda.synchronize()
+ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+t = 6
+for k in range(K):
+    ev[k][0].record(); st.evolve_zeta_(t); ev[k][1].record(); st.evolve_psi_(); ev[k][2].record(); t += 1
+torch.cuda.synchronize()
+tz = sorted(e[0].elapsed_time(e[1]) for e in ev)
+tp = sorted(e[1].elapsed_time(e[2]) for e in ev)
+gb = 96 * n * n / 1e9
+print(json.dumps({"variant": os.environ.get("QG_TEND_VARIANT", "0"), "tend_ms_med": tz[K // 2], "tend_ms_min": tz[0],
+                  "tend_TBs": gb / tz[K // 2], "solve_ms_med": tp[K // 2]}))
