@@ -119,9 +119,24 @@ int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2
 int qg_get_stats(qg_ctx *ctx, qg_stats *out);
 int qg_synchronize(qg_ctx *ctx);
 
-/* ---- multi-GPU (one rank per GPU, slab decomposition in y) --------------------------- */
+/* ---- multi-GPU (one rank per GPU, slab decomposition in y) ---------------------------
+ * Rank r owns global rows [r*P, (r+1)*P) of a global M x (nranks*P) grid; the y direction is
+ * periodic over the ring of ranks.  Per step the library exchanges halo rows with the two
+ * ring neighbours and all-gathers one small record per rank (the spectral solver's
+ * cross-slab carries); both go through the transport set up here.                       */
 int qg_comm_unique_id(char out[128]);               /* ncclGetUniqueId on rank 0          */
-int qg_comm_init(qg_ctx *ctx, int nranks, int rank, const char id[128]);
+int qg_comm_init(qg_ctx *ctx, int nranks, int rank, const char id[128]);  /* RCCL          */
+/* Host-provided transport (MPI, tests, ...).  Both callbacks receive DEVICE pointers and the
+ * stream the library works on; they must complete the transfer in stream order (e.g.
+ * synchronise the stream, copy, exchange, copy back) and return 0 on success.
+ * sendrecv: one grouped exchange of ns sends and nr receives (peer = rank index); messages
+ * between the same pair of ranks match in posting order.                                 */
+typedef int (*qg_allgather_fn)(void *user, const double *send, double *recv, int64_t count, void *stream);
+typedef int (*qg_sendrecv_fn)(void *user, int ns, const double *const *send, const int64_t *send_count,
+                              const int *send_peer, int nr, double *const *recv, const int64_t *recv_count,
+                              const int *recv_peer, void *stream);
+int qg_comm_init_host(qg_ctx *ctx, int nranks, int rank, qg_allgather_fn allgather, qg_sendrecv_fn sendrecv,
+                      void *user);
 
 /* ---- solver handle: the get_*_cholesky analogue --------------------------------------
  * Solves, for s = 0, 1,   A_s x_s = g_s  with A_s = construct_spA(M, P, dx, alpha[s])

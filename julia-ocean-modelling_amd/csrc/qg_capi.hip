@@ -15,6 +15,7 @@ int comm_allgather(void *user, const double *send, double *recv, int64_t count, 
 int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
               hipStream_t s);
 int comm_init(void **comm, int nranks, int rank, const char id[128]);
+int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sendrecv_fn sr, void *user);
 int comm_unique_id(char out[128]);
 }  // namespace qg
 
@@ -35,6 +36,7 @@ struct qg_ctx {
     int heads[3] = {0, 0, 0};  // physical slot of logical slot 1 for zeta, psi, f_store
     bool initialised = false;
     int rank = 0, nranks = 1;
+    bool distributed = false;    // a transport is attached: halo exchange + record gather path
     void *comm = nullptr;        // RCCL communicator wrapper (multi-GPU)
     double *halo = nullptr;      // received halo rows (multi-GPU)
     std::unique_ptr<SpectralSolver> spec;
@@ -178,7 +180,6 @@ static void fill_wrap_rows(const qg_ctx *c, const double *base, RowSrc &rs) {
 int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     if (!c || timestep < 1) return QG_ERR_INVALID_ARG;
     if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
-    if (c->nranks > 1 && !c->comm) return QG_ERR_RCCL;
     const qg_params &p = c->p;
     QG_HIP(hipSetDevice(c->device));
     const int zh = c->heads[0], ph = c->heads[1], fh = c->heads[2];
@@ -197,7 +198,7 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     a.ab3 = timestep >= 3;
     a.j0 = 0;
     a.j1 = (int)p.P;
-    a.write_ghost_rows = c->nranks == 1;
+    a.write_ghost_rows = !c->distributed;
     for (int l = 0; l < 2; ++l) {
         a.zeta[l] = c->field(c->zeta, l, zh);
         a.psi[l] = c->field(c->psi, l, ph);
@@ -206,7 +207,7 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
         a.zeta_out[l] = c->field(c->zeta, l, zn);
         a.f_out[l] = c->field(c->fst, l, fn);
     }
-    if (c->nranks == 1) {
+    if (!c->distributed) {
         for (int l = 0; l < 2; ++l) {
             fill_wrap_rows(c, a.zeta[l], a.zeta_rows[l]);
             fill_wrap_rows(c, a.psi[l], a.psi_rows[l]);
@@ -224,7 +225,7 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
             }
     }
     QG_CHECK(launch_tendency(a, c->stream));
-    if (c->nranks > 1) {  // ghost rows of the new zeta and F from the neighbours
+    if (c->distributed) {  // ghost rows of the new zeta and F from the neighbours
         double *fields[4] = {a.zeta_out[0], a.zeta_out[1], a.f_out[0], a.f_out[1]};
         QG_CHECK(comm_halo(c->comm, fields, 4, p.M, p.P, -1, nullptr, c->stream));
     }
@@ -237,13 +238,12 @@ int qg_evolve_psi(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
     if (!c->spec) return QG_ERR_UNSUPPORTED;
-    if (c->nranks > 1 && !c->comm) return QG_ERR_RCCL;
     QG_HIP(hipSetDevice(c->device));
     const int zh = c->heads[0], pn = (c->heads[1] + 2) % 3;
     double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);
-    QG_CHECK(c->spec->solve(c->field(c->zeta, 0, zh), c->field(c->zeta, 1, zh), o1, o2, c->nranks == 1, c->stream,
-                            c->nranks > 1 ? comm_allgather : nullptr, c->comm));
-    if (c->nranks > 1) {  // ghost rows of the new psi from the neighbours (drop-in ghost ring)
+    QG_CHECK(c->spec->solve(c->field(c->zeta, 0, zh), c->field(c->zeta, 1, zh), o1, o2, !c->distributed, c->stream,
+                            c->distributed ? comm_allgather : nullptr, c->comm));
+    if (c->distributed) {  // ghost rows of the new psi from the neighbours (drop-in ghost ring)
         double *fields[2] = {o1, o2};
         QG_CHECK(comm_halo(c->comm, fields, 2, c->p.M, c->p.P, -1, nullptr, c->stream));
     }
@@ -312,6 +312,14 @@ int qg_comm_unique_id(char out[128]) {
     return comm_unique_id(out);
 }
 
+static int comm_attach(qg_ctx *c, int nranks, int rank) {
+    c->rank = rank;
+    c->nranks = nranks;
+    c->distributed = true;  // also for nranks == 1: the ring then wraps onto itself
+    if (!c->halo) QG_HIP(hipMalloc((void **)&c->halo, sizeof(double) * 16 * (size_t)(c->p.M + 2)));
+    return build_solver(c);
+}
+
 int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return QG_ERR_INVALID_ARG;
     QG_HIP(hipSetDevice(c->device));
@@ -320,10 +328,19 @@ int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
         c->comm = nullptr;
     }
     QG_CHECK(comm_init(&c->comm, nranks, rank, id));
-    c->rank = rank;
-    c->nranks = nranks;
-    if (!c->halo) QG_HIP(hipMalloc((void **)&c->halo, sizeof(double) * 16 * (size_t)(c->p.M + 2)));
-    return build_solver(c);
+    return comm_attach(c, nranks, rank);
+}
+
+int qg_comm_init_host(qg_ctx *c, int nranks, int rank, qg_allgather_fn allgather, qg_sendrecv_fn sendrecv,
+                      void *user) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks || !allgather || !sendrecv) return QG_ERR_INVALID_ARG;
+    QG_HIP(hipSetDevice(c->device));
+    if (c->comm) {
+        comm_destroy(c->comm);
+        c->comm = nullptr;
+    }
+    QG_CHECK(comm_init_host(&c->comm, nranks, rank, allgather, sendrecv, user));
+    return comm_attach(c, nranks, rank);
 }
 
 // ---- solver handles ---------------------------------------------------------------------

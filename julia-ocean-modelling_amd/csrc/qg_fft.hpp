@@ -78,10 +78,9 @@ struct LdsSize {
 };
 
 template <int N, int T, int R, int NS, bool INV>
-__device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__restrict__ tw) {
+__device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__restrict__ tw, int t) {
     constexpr int NB = N / R;                 // butterflies in this pass
     constexpr int PER = (NB + T - 1) / T;     // per thread
-    const int t = threadIdx.x;
     double2 v[PER][R];
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
@@ -119,19 +118,28 @@ __device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__res
 }
 
 template <int N, int T, int NS, bool INV>
-__device__ __forceinline__ void fft_passes(double2 *buf, const double2 *__restrict__ tw) {
+__device__ __forceinline__ void fft_passes(double2 *buf, const double2 *__restrict__ tw, int t) {
     if constexpr (NS < N) {
         constexpr int R = PassRadix<N, T, NS>::value;
-        stockham_pass<N, T, R, NS, INV>(buf, tw);
-        fft_passes<N, T, NS * R, INV>(buf, tw);
+        stockham_pass<N, T, R, NS, INV>(buf, tw, t);
+        fft_passes<N, T, NS * R, INV>(buf, tw, t);
     }
+}
+
+// threadIdx.x laundered through an opaque move: the FFT's LDS addresses and twiddle indices
+// are row-invariant, and without this the compiler hoists all of them (several passes' worth)
+// out of the caller's row loop and keeps them live in VGPRs
+__device__ __forceinline__ int opaque_tid() {
+    int t;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+    return t;
 }
 
 // Unnormalised DFT of buf[lpad(0..N)) in place (natural order in and out).  Caller must have
 // synchronised after writing buf; returns after a barrier.
 template <int N, int T, bool INV>
 __device__ __forceinline__ void fft_lds(double2 *buf, const double2 *__restrict__ tw) {
-    fft_passes<N, T, 1, INV>(buf, tw);
+    fft_passes<N, T, 1, INV>(buf, tw, opaque_tid());
 }
 
 }  // namespace qg

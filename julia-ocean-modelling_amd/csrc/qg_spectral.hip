@@ -570,7 +570,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const size_t n_dc = align_up(sizeof(double) * a.Nc);
     const int64_t RS = rec_size(KS, P);
     const size_t n_rec = align_up(sizeof(double) * RS);
-    const size_t n_grec = nranks > 1 ? align_up(sizeof(double) * RS * nranks) : 0;
+    const size_t n_grec = align_up(sizeof(double) * RS * nranks);  // gather target (also 1-rank ring)
     const size_t n_ext = align_up(sizeof(double2) * 4 * KS);
     const size_t n_line = align_up(sizeof(double) * P);
     const size_t n_scal = align_up(sizeof(double) * 8);
@@ -591,7 +591,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.WIN = (double2 *)take(n_S);
     a.dcpart = (double *)take(n_dc);
     a.rec = (double *)take(n_rec);
-    grec_buf_ = nranks > 1 ? (double *)take(n_grec) : nullptr;
+    grec_buf_ = (double *)take(n_grec);
     a.grec = nranks > 1 ? grec_buf_ : a.rec;
     a.rec_stride = RS;
     a.EXT = (double2 *)take(n_ext);
@@ -626,6 +626,8 @@ int SpectralSolver::solve(const double *in1, const double *in2, double *out1, do
     QG_LAUNCH_CHECK();
     if (a.nranks > 1) {
         if (!gather) return QG_ERR_RCCL;
+        QG_CHECK(gather(user, a.rec, grec_buf_, a.rec_stride, s));
+    } else if (gather) {  // one-rank ring: still drive the transport (grec aliases rec)
         QG_CHECK(gather(user, a.rec, grec_buf_, a.rec_stride, s));
     }
     spec_pin<<<1, PIN_THREADS, 0, s>>>(a);

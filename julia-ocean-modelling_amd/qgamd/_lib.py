@@ -39,6 +39,12 @@ class QgStats(C.Structure):
                 ("pin", C.c_double)]
 
 
+# host-transport callbacks (qg_allgather_fn, qg_sendrecv_fn)
+AllgatherFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p)
+SendrecvFn = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64),
+                         C.POINTER(C.c_int), C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64),
+                         C.POINTER(C.c_int), C.c_void_p)
+
 # (name, restype, argtypes) of every symbol include/qg_mi355.h declares
 _vp, _dp, _i64, _i32 = C.c_void_p, C.c_void_p, C.c_int64, C.c_int
 SIGNATURES = [
@@ -60,6 +66,7 @@ SIGNATURES = [
     ("qg_synchronize", C.c_int, [_vp]),
     ("qg_comm_unique_id", C.c_int, [C.c_char_p]),
     ("qg_comm_init", C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
+    ("qg_comm_init_host", C.c_int, [_vp, C.c_int, C.c_int, AllgatherFn, SendrecvFn, _vp]),
     ("qg_solver_create", C.c_int, [_i64, _i64, C.c_double, C.c_double * 2, C.c_int * 2,
                                    C.c_double * 4, C.c_double * 4, C.c_int, C.c_int, C.c_int, _vp,
                                    C.POINTER(_vp)]),

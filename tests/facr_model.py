@@ -1,0 +1,147 @@
+"""Numpy model of the device spectral (FACR) solver -- test infrastructure.
+
+Mirrors, step for step, what julia-ocean-modelling_amd/csrc/qg_spectral.hip computes for one
+rank: x-DFT of z = f1 + i f2 per row, chunk-local backward filter u_j = cs F_j + r u_{j+1}
+with the two chunk summaries, segment scans to chunk carries, the rank record that is
+all-gathered, the cross-rank / periodic closure, the Poisson compatibility shift delta, the
+singular k = 0 Poisson line and the pin.  The checker for it is the exact DFT solve of the C
+oracle (oracle/qg_oracle.c); the kernels are checked against the oracle separately.
+"""
+import numpy as np
+
+
+def coefs(M, dx, alpha, pinned, L, Pl, Pt):
+    k = np.arange(M // 2 + 1)
+    th = 2 * np.pi * k / M
+    d = 2 * np.sin(th / 2) ** 2 - alpha * dx * dx / 2
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sq = np.sqrt(d * (d + 2))
+        r = 1 / ((1 + d) + sq)
+        lr = -np.log1p(d + sq)
+        c = dict(r=r, lr=lr, q=np.exp(L * lr), gam=r * np.expm1(2 * L * lr) / np.expm1(2 * lr),
+                 rP=np.exp(Pl * lr), gamP=r * np.expm1(2 * Pl * lr) / np.expm1(2 * lr),
+                 cs=-r * dx * dx / M, inv1mrPt=-1 / np.expm1(Pt * lr))
+    if pinned:
+        for key in c:
+            c[key] = np.array(c[key], dtype=float)
+            c[key][0] = 0.0
+    return c
+
+
+def rank_pass_a(f1, f2, M, dx, alphas, pinned0, L, Pl, Pt):
+    """Pass A + carry for one rank's slab (f1, f2: (M, Pl) interior).  Returns the record
+    (what the device all-gathers) and the per-chunk state pass B needs."""
+    Z = np.fft.fft(f1 + 1j * f2, axis=0)
+    KH = M // 2 + 1
+    kk = np.arange(KH)
+    B = [(Z[:KH] + np.conj(Z[(M - kk) % M])) / 2, (Z[:KH] - np.conj(Z[(M - kk) % M])) / (2j)]
+    Nc = Pl // L
+    st = []
+    rec = {"dsum": float(np.sum(np.real(B[0][0]))) if pinned0 else 0.0, "hline": np.real(B[0][0]).copy()}
+    for s in range(2):
+        c = coefs(M, dx, alphas[s], pinned0 and s == 0, L, Pl, Pt)
+        U = np.zeros((KH, Pl), complex)
+        ULS = np.zeros((Nc, KH), complex)
+        WLS = np.zeros((Nc, KH), complex)
+        for ch in range(Nc):
+            s0, e = ch * L, ch * L + L - 1
+            u = np.zeros(KH, complex)
+            wl = np.zeros(KH, complex)
+            wg = np.ones(KH)
+            for j in range(e, s0 - 1, -1):
+                u = c["cs"] * B[s][:, j] + c["r"] * u
+                U[:, j] = u
+                wl += wg * u
+                wg *= c["r"]
+            ULS[ch], WLS[ch] = u, wl
+        UIN = np.zeros((Nc, KH), complex)
+        WIN = np.zeros((Nc, KH), complex)
+        v = np.zeros(KH, complex)
+        for ch in range(Nc - 1, -1, -1):
+            UIN[ch] = v
+            v = ULS[ch] + c["q"] * v
+        AU = v
+        w = np.zeros(KH, complex)
+        for ch in range(Nc):
+            WIN[ch] = w
+            w = (WLS[ch] + c["gam"] * UIN[ch]) + c["q"] * w
+        AW = w
+        rec[f"AU{s}"], rec[f"AW{s}"] = AU, AW
+        if s == 0:
+            rec["ULS0"], rec["UIN0"] = ULS[0].copy(), UIN[0].copy()
+        st.append(dict(c=c, U=U, UIN=UIN, WIN=WIN))
+    return rec, st
+
+
+def rank_pass_b(recs, rank, st, M, dx, pinned0, L, Pl, Pt, P_fwd):
+    """Pin (redundantly on every rank) + pass B for one rank.  Returns (out1, out2) (M, Pl)."""
+    G = len(recs)
+    KH = M // 2 + 1
+    Nc = Pl // L
+    delta = -sum(rc["dsum"] for rc in recs) if pinned0 else 0.0
+    X = []
+    pin = 0.0
+    for s in range(2):
+        c = st[s]["c"]
+        dl = s == 0 and pinned0
+        AU = [recs[g][f"AU{s}"] + (c["cs"] * delta if dl and g == 0 else 0) for g in range(G)]
+        AW = [recs[g][f"AW{s}"] + (np.exp((Pl - 1) * c["lr"]) * c["cs"] * delta if dl and g == 0 else 0)
+              for g in range(G)]
+
+        def uext(g):
+            acc = 0
+            for m in range(G - 1, -1, -1):
+                acc = c["rP"] * acc + AU[(g + 1 + m) % G]
+            return acc * c["inv1mrPt"]
+
+        def wext(g):
+            acc = 0
+            for m in range(G - 1, -1, -1):
+                gg = (g - 1 - m) % G
+                acc = c["rP"] * acc + (AW[gg] + c["gamP"] * uext(gg))
+            return acc * c["inv1mrPt"]
+
+        with np.errstate(invalid="ignore", over="ignore"):
+            Ue, We = uext(rank), wext(rank)
+            if dl:
+                Ue0, We0 = uext(0), wext(0)
+                u0 = recs[0]["ULS0"] + c["cs"] * delta
+                uin0 = recs[0]["UIN0"] + np.exp((Nc - 1) * L * c["lr"]) * Ue0
+                w0 = (u0 + c["q"] * uin0) + c["r"] * We0
+                wt = np.where(np.arange(KH) * 2 == M, 1.0, 2.0)
+                pin = float(np.sum((wt * np.real(w0))[1:]))
+            Xs = np.zeros((KH, Pl), complex)
+            for ch in range(Nc):
+                n = ch * L
+                uin = st[s]["UIN"][ch] + np.exp((Nc - 1 - ch) * L * c["lr"]) * Ue
+                gc = np.exp((Pl - n + 1) * c["lr"]) * np.expm1(2.0 * n * c["lr"]) / np.expm1(2.0 * c["lr"]) if n > 0 else 0
+                win = st[s]["WIN"][ch] + gc * Ue + np.exp(n * c["lr"]) * We
+                if dl and rank == 0 and ch >= 1:
+                    win = win + np.exp((n - 1) * c["lr"]) * c["cs"] * delta
+                cu = c["q"] * uin
+                w = win
+                for j in range(ch * L, ch * L + L):
+                    ul = st[s]["U"][:, j].copy()
+                    if dl and rank == 0 and j == 0:
+                        ul = ul + c["cs"] * delta
+                    w = c["r"] * w + (ul + cu)
+                    with np.errstate(divide="ignore"):
+                        cu = cu / np.where(c["r"] == 0, 1, c["r"])
+                    Xs[:, j] = w
+        if dl:  # singular line over the global extent
+            h = np.concatenate([rc["hline"] for rc in recs])
+            h[0] += delta
+            S = np.cumsum(h)
+            D = S - S.mean()
+            Xl = np.concatenate([[0.0], np.cumsum(D)[:-1]]) * dx * dx / M
+            Xs[0] = Xl[rank * Pl:(rank + 1) * Pl]
+        X.append(Xs)
+    Zp = np.zeros((M, Pl), complex)
+    k = np.arange(KH)
+    Zp[k] = X[0] + 1j * X[1]
+    k2 = np.arange(1, M // 2)
+    Zp[M - k2] = np.conj(X[0][k2]) + 1j * np.conj(X[1][k2])
+    x = np.fft.ifft(Zp, axis=0) * M
+    x1, x2 = x.real - pin, x.imag
+    P_fwd = np.asarray(P_fwd)
+    return P_fwd[0, 0] * x1 + P_fwd[0, 1] * x2, P_fwd[1, 0] * x1 + P_fwd[1, 1] * x2

@@ -1,0 +1,79 @@
+"""Multi-rank (y-slab) path on the GPU: 2 and 4 ranks share the one GPU of the test box and
+exchange halo rows and solver records through the host transport (qg_comm_init_host over
+torch.distributed/gloo; RCCL itself refuses several ranks on one device).  The slabs must
+reproduce the single-GPU run of the same global model: every slot of zeta, psi and f_store,
+ghost rows included, to roundoff (the cross-slab carries reorder floating-point sums)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, M, P, steps, outdir):
+    import sys
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import qgamd
+    from qgamd.hostcomm import TorchDistTransport
+
+    m = qgamd.bench_model(M, P=P)
+    st = qgamd.State(m, P_local=P // world)
+    TorchDistTransport().attach(st, world, rank)
+    st.initialise()
+    st.run(1, steps)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"),
+             **{n: st.to_numpy(n) for n in ("zeta", "psi", "f_store")})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,M,P,steps", [(2, 64, 64, 6), (4, 32, 64, 5), (2, 128, 96, 4)])
+def test_slabs_match_single_gpu(world, M, P, steps):
+    import torch
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+
+    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps)
+    torch.cuda.synchronize()
+    g = {n: ref.to_numpy(n) for n in ("zeta", "psi", "f_store")}
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        Pl = P // world
+        for r in range(world):
+            loc = np.load(os.path.join(d, f"rank{r}.npz"))
+            for n in ("zeta", "psi", "f_store"):
+                want = g[n][:, r * Pl: r * Pl + Pl + 2]
+                err = np.linalg.norm(loc[n] - want) / np.linalg.norm(want)
+                assert err < 1e-12, (r, n, err)
