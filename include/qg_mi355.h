@@ -79,7 +79,8 @@ typedef struct qg_params {
     double P_fwd[4];
     int32_t solver;     /* qg_solver_kind (default QG_SOLVER_SPECTRAL)                  */
     int32_t precond;    /* qg_precond_kind for QG_SOLVER_PCG (default SPECTRAL)         */
-    double pcg_rtol;    /* relative residual target ||b-Ax||/||b|| (default 1e-13)      */
+    double pcg_rtol;    /* relative residual target ||b-Ax||/||b|| (default 1e-12); a   *
+                         * run that stagnates at its roundoff floor <= 1e-10 also stops */
     int32_t pcg_maxit;  /* default 500                                                  */
     int32_t chunk_rows; /* y-chunk of the spectral solver; 0 = automatic                */
 } qg_params;

@@ -7,6 +7,7 @@
 #include <new>
 
 #include "qg_common.hpp"
+#include "qg_pcg.hpp"
 #include "qg_spectral.hpp"
 
 namespace qg {
@@ -23,6 +24,7 @@ using namespace qg;
 
 struct qg_solver {
     SpectralSolver spec;
+    std::unique_ptr<PcgSolver> pcg;
     hipStream_t stream = nullptr;
     int device = 0;
 };
@@ -40,6 +42,8 @@ struct qg_ctx {
     void *comm = nullptr;        // RCCL communicator wrapper (multi-GPU)
     double *halo = nullptr;      // received halo rows (multi-GPU)
     std::unique_ptr<SpectralSolver> spec;
+    std::unique_ptr<PcgSolver> pcg;
+    int last_status = QG_OK;  // of the last solve (PCG: QG_ERR_NOT_CONVERGED is kept here)
     size_t F = 0;  // doubles per (M+2, P+2) field
 
     double *field(double *base, int layer, int slot) const { return base + F * (size_t)(layer + 2 * slot); }
@@ -72,7 +76,7 @@ void qg_default_params(qg_params *p) {
     p->P_fwd[3] = 1.0;
     p->solver = QG_SOLVER_SPECTRAL;
     p->precond = QG_PRECOND_SPECTRAL;
-    p->pcg_rtol = 1e-13;
+    p->pcg_rtol = 1e-12;
     p->pcg_maxit = 500;
     p->chunk_rows = 0;
 }
@@ -87,11 +91,19 @@ static int check_params(const qg_params *p) {
 
 static int build_solver(qg_ctx *c) {
     const qg_params &p = c->p;
-    if (p.solver != QG_SOLVER_SPECTRAL) return QG_ERR_UNSUPPORTED;
-    if (!SpectralSolver::supports(p.M, p.P)) return QG_ERR_UNSUPPORTED;
-    auto s = std::make_unique<SpectralSolver>();
     const double alpha[2] = {0.0, c->d.Seig};
     QG_HIP(hipSetDevice(c->device));
+    c->spec.reset();
+    c->pcg.reset();
+    if (p.solver == QG_SOLVER_PCG) {
+        auto s = std::make_unique<PcgSolver>();
+        QG_CHECK(s->init(p.M, p.P, p.P * c->nranks, c->rank, c->nranks, p.dx, alpha, 1, c->d.Pinv, p.P_fwd,
+                         p.precond, p.pcg_rtol, p.pcg_maxit, p.chunk_rows));
+        c->pcg = std::move(s);
+        return QG_OK;
+    }
+    if (!SpectralSolver::supports(p.M, p.P)) return QG_ERR_UNSUPPORTED;
+    auto s = std::make_unique<SpectralSolver>();
     QG_CHECK(s->init(p.M, p.P, p.P * c->nranks, c->rank, c->nranks, p.dx, alpha, 1, c->d.Pinv, p.P_fwd,
                      p.chunk_rows));
     c->spec = std::move(s);
@@ -237,18 +249,27 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
 int qg_evolve_psi(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
-    if (!c->spec) return QG_ERR_UNSUPPORTED;
+    if (!c->spec && !c->pcg) return QG_ERR_UNSUPPORTED;
     QG_HIP(hipSetDevice(c->device));
     const int zh = c->heads[0], pn = (c->heads[1] + 2) % 3;
     double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);
-    QG_CHECK(c->spec->solve(c->field(c->zeta, 0, zh), c->field(c->zeta, 1, zh), o1, o2, !c->distributed, c->stream,
-                            c->distributed ? comm_allgather : nullptr, c->comm));
+    const double *z1 = c->field(c->zeta, 0, zh), *z2 = c->field(c->zeta, 1, zh);
+    if (c->pcg) {
+        const int st = c->pcg->solve(z1, z2, o1, o2, !c->distributed, c->stream,
+                                     c->distributed ? comm_allgather : nullptr, c->comm,
+                                     c->distributed ? comm_halo : nullptr, c->comm);
+        c->last_status = st;
+        if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
+    } else {
+        QG_CHECK(c->spec->solve(z1, z2, o1, o2, !c->distributed, c->stream,
+                                c->distributed ? comm_allgather : nullptr, c->comm));
+    }
     if (c->distributed) {  // ghost rows of the new psi from the neighbours (drop-in ghost ring)
         double *fields[2] = {o1, o2};
         QG_CHECK(comm_halo(c->comm, fields, 2, c->p.M, c->p.P, -1, nullptr, c->stream));
     }
     c->heads[1] = pn;
-    return QG_OK;
+    return c->pcg ? c->last_status : QG_OK;
 }
 
 int qg_step(qg_ctx *c, int64_t timestep) {
@@ -289,6 +310,12 @@ int qg_get_stats(qg_ctx *c, qg_stats *out) {
     if (!c || !out) return QG_ERR_INVALID_ARG;
     std::memset(out, 0, sizeof(*out));
     out->relres[0] = out->relres[1] = -1;
+    if (c->pcg) {
+        out->iters[0] = out->iters[1] = c->pcg->iterations();
+        out->relres[0] = c->pcg->relres(0);
+        out->relres[1] = c->pcg->relres(1);
+        return QG_OK;
+    }
     if (!c->spec) return QG_OK;
     double sc[2];
     QG_HIP(hipSetDevice(c->device));
@@ -350,7 +377,7 @@ int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], con
     (void)precond;
     if (!out || !alpha || !pinned || !proj_in || !proj_out) return QG_ERR_INVALID_ARG;
     *out = nullptr;
-    if (kind != QG_SOLVER_SPECTRAL) return QG_ERR_UNSUPPORTED;
+    if (kind != QG_SOLVER_SPECTRAL && kind != QG_SOLVER_PCG) return QG_ERR_INVALID_ARG;
     if (pinned[1]) return QG_ERR_UNSUPPORTED;           // only system 0 may be the pinned Poisson
     if (pinned[0] && alpha[0] != 0.0) return QG_ERR_INVALID_ARG;
     qg_solver *s = new (std::nothrow) qg_solver();
@@ -361,7 +388,14 @@ int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], con
         delete s;
         return QG_ERR_HIP;
     }
-    const int st = s->spec.init(M, P, P, 0, 1, dx, alpha, pinned[0], proj_in, proj_out, 0);
+    int st;
+    if (kind == QG_SOLVER_PCG) {
+        // CG on -A with b = -(proj_in f): the same x as A x = proj_in f
+        s->pcg = std::make_unique<PcgSolver>();
+        st = s->pcg->init(M, P, P, 0, 1, dx, alpha, pinned[0], proj_in, proj_out, precond, 1e-13, 4000, 0);
+    } else {
+        st = s->spec.init(M, P, P, 0, 1, dx, alpha, pinned[0], proj_in, proj_out, 0);
+    }
     if (st != QG_OK) {
         delete s;
         return st;
@@ -373,6 +407,7 @@ int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], con
 int qg_solver_solve(qg_solver *s, const double *f_1, const double *f_2, double *out_1, double *out_2) {
     if (!s || !f_1 || !out_1) return QG_ERR_INVALID_ARG;
     QG_HIP(hipSetDevice(s->device));
+    if (s->pcg) return s->pcg->solve(f_1, f_2, out_1, out_2, 1, s->stream);
     return s->spec.solve(f_1, f_2, out_1, out_2, 1, s->stream);
 }
 

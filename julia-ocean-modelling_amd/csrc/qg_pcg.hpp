@@ -1,0 +1,52 @@
+// Matrix-free PCG solver for the evolve_psi! pair of systems (see qg_pcg.hip).
+#pragma once
+
+#include "qg_common.hpp"
+#include "qg_spectral.hpp"
+
+namespace qg {
+
+// device scalar slots (per system s: +s)
+enum { PCG_BB = 0, PCG_RZ = 2, PCG_ALPHA = 4, PCG_BETA = 6, PCG_RR = 8, PCG_RSUM = 10, PCG_NSCAL = 12 };
+
+struct PcgArgs {
+    int64_t M, P, ld, P_total, j_offset;
+    int rank, nranks;
+    double idx2;
+    double alpha[2];
+    int pinned0;
+    double proj_in[4], proj_out[4];
+    int ghost_rows;
+    const double *in1, *in2;
+    double *out1, *out2;
+    double *x[2], *r[2], *p[2], *q[2], *z[2];  // (M+2, P+2) fields
+    double *partial;                            // [blocks][2]
+    double *scal;                               // PCG_NSCAL doubles
+};
+
+class PcgSolver {
+public:
+    typedef int (*HaloFn)(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth,
+                          double *halo_buf, hipStream_t s);
+    int init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks, double dx, const double alpha[2],
+             int pinned0, const double proj_in[4], const double proj_out[4], int precond, double rtol, int maxit,
+             int chunk_rows);
+    ~PcgSolver();
+    // Synchronises the stream once per iteration (convergence test on the host).
+    int solve(const double *in1, const double *in2, double *out1, double *out2, int ghost_rows, hipStream_t s,
+              SpectralSolver::GatherFn gather = nullptr, void *user = nullptr, HaloFn halo = nullptr,
+              void *halo_user = nullptr);
+    int iterations() const { return iters_; }
+    double relres(int s) const { return relres_[s]; }
+
+private:
+    int reduce(int what, hipStream_t s, SpectralSolver::GatherFn gather, void *user);
+    PcgArgs a_{};
+    SpectralSolver pre_;
+    int precond_ = 0, maxit_ = 500, nblk_ = 0, iters_ = 0;
+    double rtol_ = 1e-13, relres_[2] = {-1, -1};
+    void *mem_ = nullptr;
+    double *gathered_ = nullptr;
+};
+
+}  // namespace qg

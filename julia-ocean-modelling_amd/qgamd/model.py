@@ -116,7 +116,8 @@ def P_inv_matrix(m):  # model.jl:90-99
     return (1 / (a + b)) * np.array([[b, a], [-b, b]])
 
 
-def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_local=None):
+def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_local=None,
+              precond=_lib.QG_PRECOND_SPECTRAL, pcg_rtol=1e-12, pcg_maxit=500):
     p = QgParams()
     _lib.lib().qg_default_params(C.byref(p))
     for n in ("H_1", "H_2", "beta", "Lx", "Ly", "dt", "T", "U", "dx", "visc", "r", "R_d",
@@ -128,6 +129,9 @@ def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_loc
         for k, v in enumerate(np.asarray(P_fwd, dtype=np.float64).reshape(-1)):
             p.P_fwd[k] = float(v)
     p.solver = int(solver)
+    p.precond = int(precond)
+    p.pcg_rtol = float(pcg_rtol)
+    p.pcg_maxit = int(pcg_maxit)
     p.chunk_rows = int(chunk_rows)
     return p
 
@@ -174,7 +178,8 @@ class State:
     """
 
     def __init__(self, m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0,
-                 device=None, rank=0, nranks=1, P_local=None):
+                 device=None, rank=0, nranks=1, P_local=None, precond=_lib.QG_PRECOND_SPECTRAL,
+                 pcg_rtol=1e-12, pcg_maxit=500):
         torch = _torch()
         self.model = m
         self.P_local = m.P if P_local is None else P_local
@@ -182,7 +187,7 @@ class State:
         self.zeta = device_zeros(m, self.P_local)
         self.psi = device_zeros(m, self.P_local)
         self.f_store = device_zeros(m, self.P_local)
-        self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local)
+        self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local, precond, pcg_rtol, pcg_maxit)
         self._ctx = C.c_void_p()
         call("qg_create", C.byref(self.params), int(self.device), _stream_ptr(), C.byref(self._ctx))
         call("qg_bind_state", self._ctx, _ptr(self.zeta), _ptr(self.psi), _ptr(self.f_store))
@@ -350,13 +355,13 @@ class PairSolver:
     """qg_solver handle: A_s x_s = proj_in . f for s = 0 (optionally pinned Poisson), 1."""
 
     def __init__(self, M, P, dx, alpha, pinned=(0, 0), proj_in=(1, 0, 0, 1), proj_out=(1, 0, 0, 1),
-                 kind=_lib.QG_SOLVER_SPECTRAL):
+                 kind=_lib.QG_SOLVER_SPECTRAL, precond=_lib.QG_PRECOND_SPECTRAL):
         torch = _torch()
         self.M, self.P = M, P
         self._h = C.c_void_p()
         call("qg_solver_create", int(M), int(P), float(dx), (C.c_double * 2)(*alpha),
              (C.c_int * 2)(*pinned), (C.c_double * 4)(*proj_in), (C.c_double * 4)(*proj_out),
-             int(kind), 1, int(torch.cuda.current_device()), _stream_ptr(), C.byref(self._h))
+             int(kind), int(precond), int(torch.cuda.current_device()), _stream_ptr(), C.byref(self._h))
 
     def solve(self, f1, f2=None, out1=None, out2=None):
         torch = _torch()
@@ -372,13 +377,13 @@ class PairSolver:
             self._h = None
 
 
-def sp_solve_modified_helmholtz(M, P, dx, f, alpha):
+def sp_solve_modified_helmholtz(M, P, dx, f, alpha, **kw):
     """laplacian.jl:78-86: solution x of construct_spA(M,P,dx,alpha) x = f, with ghosts."""
-    s = PairSolver(M, P, dx, (float(alpha), -1.0), (0, 0), (1, 0, 0, 0), (1, 0, 0, 0))
+    s = PairSolver(M, P, dx, (float(alpha), -1.0), (0, 0), (1, 0, 0, 0), (1, 0, 0, 0), **kw)
     return s.solve(f)
 
 
-def sp_solve_poisson(M, P, dx, f):
+def sp_solve_poisson(M, P, dx, f, **kw):
     """laplacian.jl:100-111: the pinned Poisson solve (x = 0 at interior (1,1))."""
-    s = PairSolver(M, P, dx, (0.0, -1.0), (1, 0), (1, 0, 0, 0), (1, 0, 0, 0))
+    s = PairSolver(M, P, dx, (0.0, -1.0), (1, 0), (1, 0, 0, 0), (1, 0, 0, 0), **kw)
     return s.solve(f)
