@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--n", type=int, default=4096, help="grid points per side per GPU")
     ap.add_argument("--dt", type=float, default=60.0)
     ap.add_argument("--chunk-rows", type=int, default=0)
-    ap.add_argument("--cpu-steps", type=int, default=3, help="CPU-oracle sample steps (0 = skip)")
+    ap.add_argument("--cpu-steps", type=int, default=10, help="CPU-oracle sample steps (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all threads OpenMP offers")
     return ap.parse_args()
 

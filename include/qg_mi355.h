@@ -101,6 +101,8 @@ const char *qg_strerror(int status);
 void qg_default_params(qg_params *p);
 
 /* ---- model context (replaces the state arrays + the two CHOLMOD factors) ------------ */
+/* replaces BaroclinicModel(...) + get_poisson_cholesky / get_helmholtz_cholesky
+ * (model.jl:12-34, laplacian.jl:60-75, called at run_model_no_output.jl:5-6)        */
 int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out);
 int qg_destroy(qg_ctx *ctx);
 /* zeta, psi, f_store: device (M+2, P+2, 2, 3) Float64 arrays owned by the caller */
@@ -109,15 +111,17 @@ int qg_bind_state(qg_ctx *ctx, double *zeta, double *psi, double *f_store);
  * kick*U*Ly*u01(seed_l, i + M*j_global); zeroes all other slots and f_store; resets the
  * slot rotation. */
 int qg_initialise(qg_ctx *ctx, uint64_t seed1, uint64_t seed2);
-int qg_evolve_zeta(qg_ctx *ctx, int64_t timestep); /* 1-based; Euler for 1, 2, AB3 after */
-int qg_evolve_psi(qg_ctx *ctx);
-int qg_step(qg_ctx *ctx, int64_t timestep);        /* evolve_zeta! then evolve_psi!       */
-int qg_run(qg_ctx *ctx, int64_t first_step, int64_t nsteps);
+int qg_evolve_zeta(qg_ctx *ctx, int64_t timestep); /* evolve_zeta! model.jl:155-170; 1-based */
+int qg_evolve_psi(qg_ctx *ctx);                    /* evolve_psi! model.jl:172-199        */
+int qg_step(qg_ctx *ctx, int64_t timestep);        /* the pair run_model_no_output.jl:11-12 */
+int qg_run(qg_ctx *ctx, int64_t first_step, int64_t nsteps); /* loop run_model_no_output.jl:10-13 */
 /* which: 0 = zeta, 1 = psi, 2 = f_store; logical 1..3 -> physical 0..2 */
 int qg_slot(const qg_ctx *ctx, int which, int logical, int *physical);
 int qg_set_slots(qg_ctx *ctx, const int heads[3]); /* restore a saved rotation (resume)  */
 int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2,3       */
 int qg_get_stats(qg_ctx *ctx, qg_stats *out);
+/* the same, flattened (no struct): PCG iterations and relative residuals of the last solve */
+int qg_solver_stats(qg_ctx *ctx, int *it_poisson, int *it_helm, double *relres_p, double *relres_h);
 int qg_synchronize(qg_ctx *ctx);
 
 /* ---- multi-GPU (one rank per GPU, slab decomposition in y) ---------------------------
@@ -150,15 +154,16 @@ int qg_comm_init_host(qg_ctx *ctx, int nranks, int rank, qg_allgather_fn allgath
 int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], const int pinned[2],
                      const double proj_in[4], const double proj_out[4], int kind, int precond,
                      int device, void *stream, qg_solver **out);
+/* the `factor \ b` of sp_solve_* (laplacian.jl:78-111) / model.jl:186,191 */
 int qg_solver_solve(qg_solver *s, const double *f_1, const double *f_2, double *out_1, double *out_2);
 int qg_solver_destroy(qg_solver *s);
 
 /* ---- stateless kernels on (M+2, P+2) device fields (ghost ring refreshed on output) ---- */
-int qg_laplace_5p(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream);
-int qg_cd(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream);
+int qg_laplace_5p(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream); /* laplacian.jl:15-27 */
+int qg_cd(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream);          /* model.jl:68-80 */
 int qg_arakawa_J(const double *zeta, const double *psi, double *out, int64_t M, int64_t P,
-                 double dx, void *stream);
-int qg_fill_ghosts(double *b, int64_t M, int64_t P, void *stream);
+                 double dx, void *stream);                             /* J, arakawa.jl:7-62 */
+int qg_fill_ghosts(double *b, int64_t M, int64_t P, void *stream); /* boundary_conditions.jl:2-13 */
 
 #ifdef __cplusplus
 }

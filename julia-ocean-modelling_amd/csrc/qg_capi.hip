@@ -326,6 +326,17 @@ int qg_get_stats(qg_ctx *c, qg_stats *out) {
     return QG_OK;
 }
 
+int qg_solver_stats(qg_ctx *c, int *it_poisson, int *it_helm, double *relres_p, double *relres_h) {
+    qg_stats st;
+    const int rc = qg_get_stats(c, &st);
+    if (rc != QG_OK) return rc;
+    if (it_poisson) *it_poisson = st.iters[0];
+    if (it_helm) *it_helm = st.iters[1];
+    if (relres_p) *relres_p = st.relres[0];
+    if (relres_h) *relres_h = st.relres[1];
+    return QG_OK;
+}
+
 int qg_synchronize(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     QG_HIP(hipSetDevice(c->device));

@@ -1,0 +1,215 @@
+"""
+    QGMI355
+
+Julia host side of the MI355X hot path: the reference's operator surface
+(`evolve_zeta!`, `evolve_psi!`, `run_model_no_output`, `get_poisson_cholesky`,
+`get_helmholtz_cholesky`, `J`, `laplace_5p`, `cd`, `update_doubly_periodic_bc!`) specialised
+on device arrays, each method a thin `ccall` into `libqgmi355.so` (include/qg_mi355.h).
+AMDGPU.jl supplies only device memory (`ROCArray`) and the stream handle.
+
+Reference methods replaced (JSLeadbetter/julia-ocean-modelling @ 2024-10-08):
+  evolve_zeta!           src/model.jl:155-170
+  evolve_psi!            src/model.jl:172-199   (CHOLMOD factors -> `QGSolverPair` handle)
+  get_poisson_cholesky   src/schemes/laplacian.jl:66-75
+  get_helmholtz_cholesky src/schemes/laplacian.jl:60-64
+  run_model_no_output    src/run_model_no_output.jl:3-16
+  initialise_model       src/model.jl:37-62     (seeded, on the device)
+  J / laplace_5p / cd    src/schemes/arakawa.jl:58-62, laplacian.jl:15-27, model.jl:68-80
+
+This file is not exercised in this repository's CI (the build image has no Julia); the
+same C-ABI calls are exercised from Python (qgamd/_lib.py) by tests/. See INTEGRATION.md.
+"""
+module QGMI355
+
+using AMDGPU
+
+const libqg = get(ENV, "QGMI355_LIB", joinpath(@__DIR__, "..", "lib", "libqgmi355.so"))
+
+# --- qg_params (include/qg_mi355.h), field order and padding identical to the C struct ----
+struct QGParams
+    H_1::Float64; H_2::Float64; beta::Float64; Lx::Float64; Ly::Float64
+    dt::Float64; T::Float64; U::Float64
+    M::Int64; P::Int64
+    dx::Float64; visc::Float64; r::Float64; R_d::Float64; initial_kick::Float64
+    P_fwd::NTuple{4,Float64}
+    solver::Int32; precond::Int32
+    pcg_rtol::Float64
+    pcg_maxit::Int32; chunk_rows::Int32
+end
+
+struct QGStats
+    iters::NTuple{2,Int32}
+    relres::NTuple{2,Float64}
+    delta::Float64
+    pin::Float64
+end
+
+const SOLVER_SPECTRAL = Int32(0)
+const SOLVER_PCG = Int32(1)
+
+struct QGError <: Exception
+    fn::Symbol
+    status::Cint
+end
+Base.showerror(io::IO, e::QGError) =
+    print(io, "$(e.fn) failed: ", unsafe_string(ccall((:qg_strerror, libqg), Cstring, (Cint,), e.status)))
+
+macro qgcheck(fn, ex)
+    quote
+        local st = $(esc(ex))
+        st == 0 || throw(QGError($(QuoteNode(fn)), st))
+        nothing
+    end
+end
+
+stream_ptr() = AMDGPU.stream().stream   # hipStream_t of the task-local stream
+
+"""Parameters of a reference `BaroclinicModel` (model.jl:12-30) in the C struct."""
+function QGParams(model; P_local::Integer=model.P, solver=SOLVER_SPECTRAL, P_fwd=(1.0, -1.0, 1.0, 1.0),
+                  precond::Integer=1, pcg_rtol=1e-12, pcg_maxit::Integer=500, chunk_rows::Integer=0)
+    QGParams(model.H_1, model.H_2, model.beta, model.Lx, model.Ly, model.dt, model.T, model.U,
+             model.M, P_local, model.dx, model.visc, model.r, model.R_d, model.initial_kick,
+             Tuple(Float64.(P_fwd)), Int32(solver), Int32(precond), pcg_rtol, Int32(pcg_maxit),
+             Int32(chunk_rows))
+end
+
+"""
+    QGState(model; kwargs...)
+
+Device state `zeta`, `psi`, `f_store` as `(M+2, P+2, 2, 3)` `ROCArray{Float64,4}` (the
+reference's layout) plus the library context that owns the solver scratch.  History slots
+rotate instead of being copied; `canonical!(s)` restores the reference's slot order.
+"""
+mutable struct QGState
+    ctx::Ptr{Cvoid}
+    zeta::ROCArray{Float64,4}
+    psi::ROCArray{Float64,4}
+    f_store::ROCArray{Float64,4}
+end
+
+function QGState(model; P_local::Integer=model.P, kw...)
+    params = Ref(QGParams(model; P_local=P_local, kw...))
+    shape = (model.M + 2, P_local + 2, 2, 3)
+    zeta, psi, fs = AMDGPU.zeros(Float64, shape), AMDGPU.zeros(Float64, shape), AMDGPU.zeros(Float64, shape)
+    ctx = Ref{Ptr{Cvoid}}(C_NULL)
+    @qgcheck qg_create ccall((:qg_create, libqg), Cint, (Ptr{QGParams}, Cint, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                             params, AMDGPU.device_id(AMDGPU.device()) - 1, stream_ptr(), ctx)
+    @qgcheck qg_bind_state ccall((:qg_bind_state, libqg), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                                 ctx[], pointer(zeta), pointer(psi), pointer(fs))
+    s = QGState(ctx[], zeta, psi, fs)
+    finalizer(x -> ccall((:qg_destroy, libqg), Cint, (Ptr{Cvoid},), x.ctx), s)
+    s
+end
+
+"""`initialise_model(model)` (model.jl:37-62) on the device with seeded uniform noise.  For
+a multi-GPU run create the `QGState`, `comm_init!` it, then `initialise!` it (the global
+index of the noise depends on the rank)."""
+initialise!(s::QGState; seeds=(20241008, 20241009)) =
+    @qgcheck qg_initialise ccall((:qg_initialise, libqg), Cint, (Ptr{Cvoid}, UInt64, UInt64), s.ctx, seeds[1], seeds[2])
+
+function initialise_model(model; seeds=(20241008, 20241009), kw...)
+    s = QGState(model; kw...)
+    initialise!(s; seeds=seeds)
+    s
+end
+
+"""`evolve_zeta!` (model.jl:155-170): Euler for timestep 1, 2, AB3 after; both layers."""
+evolve_zeta!(model, s::QGState, timestep::Integer) =
+    @qgcheck qg_evolve_zeta ccall((:qg_evolve_zeta, libqg), Cint, (Ptr{Cvoid}, Int64), s.ctx, timestep)
+
+"""`evolve_psi!` (model.jl:172-199); the factor arguments of the reference are the context's
+solver here, so the handles are accepted for signature compatibility and ignored."""
+evolve_psi!(model, s::QGState, poisson=nothing, helmholtz=nothing) =
+    @qgcheck qg_evolve_psi ccall((:qg_evolve_psi, libqg), Cint, (Ptr{Cvoid},), s.ctx)
+
+"""`run_model_no_output(model)` (run_model_no_output.jl:3-16) -> (zeta, psi) on the device,
+slots in the reference's order."""
+function run_model_no_output(model; kw...)
+    s = initialise_model(model; kw...)
+    nsteps = floor(Int, model.T / model.dt)
+    @qgcheck qg_run ccall((:qg_run, libqg), Cint, (Ptr{Cvoid}, Int64, Int64), s.ctx, 1, nsteps)
+    canonical!(s)
+    AMDGPU.synchronize()
+    (s.zeta, s.psi)
+end
+
+canonical!(s::QGState) = @qgcheck qg_canonicalize ccall((:qg_canonicalize, libqg), Cint, (Ptr{Cvoid},), s.ctx)
+
+function stats(s::QGState)
+    r = Ref{QGStats}()
+    @qgcheck qg_get_stats ccall((:qg_get_stats, libqg), Cint, (Ptr{Cvoid}, Ptr{QGStats}), s.ctx, r)
+    r[]
+end
+
+# --- solver handles: the get_*_cholesky analogues ----------------------------------------
+mutable struct QGSolverPair
+    h::Ptr{Cvoid}
+end
+
+# One handle solves a pair of systems; a single-system handle (as the reference's factors are)
+# feeds the second system nothing (proj_in row 2 = 0) and gives it a harmless alpha = -1.
+function QGSolverPair(M, P, dx, alpha::NTuple{2,Float64}, pinned::NTuple{2,Cint};
+                      kind=SOLVER_SPECTRAL, precond=Cint(1))
+    out = Ref{Ptr{Cvoid}}(C_NULL)
+    id = (1.0, 0.0, 0.0, 0.0)
+    @qgcheck qg_solver_create ccall((:qg_solver_create, libqg), Cint,
+        (Int64, Int64, Float64, Ref{NTuple{2,Float64}}, Ref{NTuple{2,Cint}}, Ref{NTuple{4,Float64}},
+         Ref{NTuple{4,Float64}}, Cint, Cint, Cint, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+        M, P, dx, alpha, pinned, id, id, kind, precond, AMDGPU.device_id(AMDGPU.device()) - 1, stream_ptr(), out)
+    s = QGSolverPair(out[])
+    finalizer(x -> ccall((:qg_solver_destroy, libqg), Cint, (Ptr{Cvoid},), x.h), s)
+    s
+end
+
+get_poisson_cholesky(M, P, dx; kw...) = QGSolverPair(M, P, dx, (0.0, -1.0), (Cint(1), Cint(0)); kw...)
+get_helmholtz_cholesky(M, P, dx, alpha; kw...) = QGSolverPair(M, P, dx, (Float64(alpha), -1.0), (Cint(0), Cint(0)); kw...)
+
+"""`factor \\ b` on (M+2, P+2) device fields: solves A x = f (interior), ghosts refreshed."""
+function solve!(out::ROCArray{Float64,2}, s::QGSolverPair, f::ROCArray{Float64,2})
+    @qgcheck qg_solver_solve ccall((:qg_solver_solve, libqg), Cint,
+        (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+        s.h, pointer(f), C_NULL, pointer(out), C_NULL)
+    out
+end
+
+# --- stateless stencils (return new arrays, like the reference) --------------------------
+for (jl, c) in ((:laplace_5p, :qg_laplace_5p), (:cd, :qg_cd))
+    @eval function $jl(u::ROCArray{Float64,2}, dx::Float64)
+        out = similar(u)
+        M, P = size(u) .- 2
+        @qgcheck $c ccall(($(QuoteNode(c)), libqg), Cint, (Ptr{Float64}, Ptr{Float64}, Int64, Int64, Float64, Ptr{Cvoid}),
+                          pointer(u), pointer(out), M, P, dx, stream_ptr())
+        out
+    end
+end
+
+function J(dx::Float64, zeta::ROCArray{Float64,2}, psi::ROCArray{Float64,2})
+    out = similar(zeta)
+    M, P = size(zeta) .- 2
+    @qgcheck qg_arakawa_J ccall((:qg_arakawa_J, libqg), Cint,
+        (Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Int64, Int64, Float64, Ptr{Cvoid}),
+        pointer(zeta), pointer(psi), pointer(out), M, P, dx, stream_ptr())
+    out
+end
+
+function update_doubly_periodic_bc!(b::ROCArray{Float64,2})
+    M, P = size(b) .- 2
+    @qgcheck qg_fill_ghosts ccall((:qg_fill_ghosts, libqg), Cint, (Ptr{Float64}, Int64, Int64, Ptr{Cvoid}),
+                                  pointer(b), M, P, stream_ptr())
+    b
+end
+
+# --- multi-GPU: one Julia process per GPU, RCCL communicator ------------------------------
+"""`comm_init!(s, nranks, rank, id)`: `id` = 128 bytes from `unique_id()` on rank 0, shipped
+to the other ranks by the launcher (MPI.jl `MPI.Bcast!`, a file, ...)."""
+function unique_id()
+    buf = zeros(UInt8, 128)
+    @qgcheck qg_comm_unique_id ccall((:qg_comm_unique_id, libqg), Cint, (Ptr{UInt8},), buf)
+    buf
+end
+
+comm_init!(s::QGState, nranks::Integer, rank::Integer, id::Vector{UInt8}) =
+    @qgcheck qg_comm_init ccall((:qg_comm_init, libqg), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{UInt8}),
+                                s.ctx, nranks, rank, id)
+
+end # module

@@ -63,6 +63,8 @@ SIGNATURES = [
     ("qg_set_slots", C.c_int, [_vp, C.c_int * 3]),
     ("qg_canonicalize", C.c_int, [_vp]),
     ("qg_get_stats", C.c_int, [_vp, C.POINTER(QgStats)]),
+    ("qg_solver_stats", C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                  C.POINTER(C.c_double)]),
     ("qg_synchronize", C.c_int, [_vp]),
     ("qg_comm_unique_id", C.c_int, [C.c_char_p]),
     ("qg_comm_init", C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
