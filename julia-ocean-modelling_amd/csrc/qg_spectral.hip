@@ -53,18 +53,30 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
     double dc = 0;
     double *hline = a.rec + rec_HLINE(KS);
-    for (int j = e; j >= s0; --j) {
-        asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
+    // register prefetch: row j-1 is loaded while row j is transformed (the barriers only wait
+    // for LDS traffic, so the global loads stay in flight across the FFT)
+    double pf1[EP], pf2[EP];
+    auto load_row = [&](int j) {
         const double *r1 = a.in1 + fidx(1, j + 1, ld);
         const double *r2 = a.in2 + fidx(1, j + 1, ld);
 #pragma unroll
         for (int p = 0; p < EP; ++p) {
             const int i = t + p * T;
             if (N % T == 0 || i < N) {
-                const double x1 = r1[i], x2 = r2[i];
-                buf[lpad(i)] = make_double2(p0 * x1 + p1 * x2, p2 * x1 + p3 * x2);
+                pf1[p] = r1[i];
+                pf2[p] = r2[i];
             }
         }
+    };
+    load_row(e);
+    for (int j = e; j >= s0; --j) {
+        asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
+#pragma unroll
+        for (int p = 0; p < EP; ++p) {
+            const int i = t + p * T;
+            if (N % T == 0 || i < N) buf[lpad(i)] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
+        }
+        if (j > s0) load_row(j - 1);
         __syncthreads();
         fft_lds<N, T, false>(buf, a.tw);
         double2 *Urow = a.U + (size_t)j * 2 * KS;
@@ -393,7 +405,29 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             }
         }
     }
+    // register prefetch of the next row of u (in flight across this row's FFT).  Slot (0, t=0)
+    // packs the real lines k = 0 (.x) and k = N/2 (.y).
+    double2 upf[KQ][2];
+    auto load_u = [&](int j) {
+        const double2 *Urow = a.U + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+            const int k = t + q * T;
+            if (NH % T == 0 || k < NH) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    upf[q][s] = k == 0 ? make_double2(Urow[s * KS].x, Urow[s * KS + NH].x) : Urow[s * KS + k];
+            }
+        }
+    };
+    load_u(s0);
     for (int j = s0; j <= e; ++j) {
+        double2 ucur[KQ][2];
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) ucur[q][s] = upf[q][s];
+        if (j < e) load_u(j + 1);
         // compiler memory barrier: re-read the (L1-resident) coefficients every row instead of
         // hoisting them into registers, which would spill at this occupancy
         asm volatile("" ::: "memory");
@@ -401,14 +435,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
             if (NH % T == 0 || k < NH) {
-                const double2 *Urow = a.U + (size_t)j * 2 * KS;
                 double2 X[2];
                 if (k == 0) {
                     double x0[2], xN[2];
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const Coef *c0 = a.coef + s * KS, *cN = a.coef + s * KS + NH;
-                        double ul0 = Urow[s * KS].x, ulN = Urow[s * KS + NH].x;
+                        double ul0 = ucur[q][s].x, ulN = ucur[q][s].y;
                         if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
                             ul0 += c0->cs * delta;
                             ulN += cN->cs * delta;
@@ -426,7 +459,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const Coef *cf = a.coef + s * KS + k;
-                        double2 ul = Urow[s * KS + k];
+                        double2 ul = ucur[q][s];
                         if (s == 0 && inject && j == 0) ul.x += cf->cs * delta;
                         w[q][s] = cfma(cf->r, w[q][s], cadd(ul, cu[q][s]));
                         cu[q][s] = cscale(cu[q][s], cf->rinv);
