@@ -1,8 +1,21 @@
-// In-LDS complex FFT for one row of length N (power of two), executed by a whole
-// workgroup of T threads.  Stockham autosort formulation: every pass reads R values per
-// butterfly into registers, applies the twiddles, does an R-point DFT in registers and
-// writes back in natural order, so no bit-reversal pass is needed.  Twiddles come from a
-// table tw[m] = exp(-2*pi*i*m/N) (L2/L1-resident, N complex doubles).
+// In-LDS complex FFT for one row of length N (power of two), executed by a whole workgroup
+// of T threads.  Stockham autosort formulation, out of place between two LDS buffers
+// (ping-pong): every pass reads R values per butterfly, applies the twiddles, does an R-point
+// DFT in registers and writes the next buffer in natural order -- one barrier per pass and no
+// bit-reversal pass.  When one butterfly per thread covers the row (N / R == T) the first
+// pass can take its inputs from registers and the last pass can leave its outputs in
+// registers, in exactly the element order of a coalesced row access (element t + r*T), so the
+// caller's global load / store feeds the transform without an LDS round trip.
+//
+// Twiddles live in LDS (row-invariant, filled once per workgroup from the global table
+// tw[m] = exp(-2 pi i m / N)): one small table per pass, entries exp(-2 pi i k / (NS R)),
+// k < NS; passes with NS > 256 use a two-level table (64 low + NS/64 high entries, one
+// complex multiply to combine).
+//
+// LDS layouts: a pass with stride NS < 8 scatters with a lane stride of NS*16 B, which
+// conflicts in the 8-lane groups of ds_write_b128; its output buffer uses lpad (one pad slot
+// per 8 values).  All other buffers (caller-written rows, wide-stride pass outputs) are read
+// and written contiguously and use the identity layout.
 #pragma once
 
 #include "qg_common.hpp"
@@ -60,8 +73,8 @@ __device__ __forceinline__ void dftR(double2 (&v)[R]) {
     else dft8<INV>(v);
 }
 
-// radix of the next pass: 8 while the remaining length allows it and every thread still gets
-// a butterfly (or radix 4 would not fill the threads either), else 4, else 2
+// radix of the pass with stride NS: 8 while the remaining length allows it and every thread
+// still gets a butterfly (or radix 4 would not fill the threads either), else 4, else 2
 template <int N, int T, int NS>
 struct PassRadix {
     static constexpr int REM = N / NS;
@@ -69,18 +82,81 @@ struct PassRadix {
         (REM % 8 == 0 && (N / 8 >= T || N / 4 < T)) ? 8 : ((REM % 4 == 0) ? 4 : 2);
 };
 
-// LDS index with one pad slot per 8 complex values: keeps the radix-8 scatter of the first
-// pass (lane stride 8 x 16 B) free of ds_write_b128 bank conflicts.
 __host__ __device__ constexpr int lpad(int x) { return x + (x >> 3); }
+template <int NS>  // layout of the buffer written by the pass with stride NS (caller: NS = 0)
+__device__ __forceinline__ int lay(int x) {
+    if constexpr (NS > 0 && NS < 8) return lpad(x);
+    else return x;
+}
 template <int N>
-struct LdsSize {
-    static constexpr int value = lpad(N - 1) + 1;  // complex elements
+struct LdsSize {  // complex elements of one row buffer (any layout)
+    static constexpr int value = lpad(N - 1) + 1;
 };
 
-template <int N, int T, int R, int NS, bool INV>
-__device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__restrict__ tw, int t) {
-    constexpr int NB = N / R;                 // butterflies in this pass
-    constexpr int PER = (NB + T - 1) / T;     // per thread
+// pass sequence facts, by recursion over the stride NS
+template <int N, int T, int NS, bool END = (NS >= N)>
+struct Passes {
+    static constexpr int R = PassRadix<N, T, NS>::value;
+    using Next = Passes<N, T, NS * R>;
+    static constexpr int count = 1 + Next::count;
+    static constexpr int last_ns = (NS * R >= N) ? NS : Next::last_ns;
+    static constexpr int tw_here = NS == 1 ? 0 : (NS <= 256 ? NS : 64 + NS / 64);
+    static constexpr int tw_total = tw_here + Next::tw_total;  // this pass and the later ones
+};
+template <int N, int T, int NS>
+struct Passes<N, T, NS, true> {
+    static constexpr int count = 0, last_ns = 0, tw_here = 0, tw_total = 0;
+};
+
+template <int N, int T>
+struct FftPlan {
+    using P = Passes<N, T, 1>;
+    static constexpr int R0 = P::R;
+    static constexpr int NPASS = P::count;
+    static constexpr int LAST_NS = P::last_ns;
+    static constexpr int R_LAST = N / LAST_NS;
+    static constexpr int TW = P::tw_total;
+    // one butterfly per thread in the first / last pass, in row order t + r*T
+    static constexpr bool REG_IN = (N / R0 == T);
+    static constexpr bool REG_OUT = (N / R_LAST == T);
+    static constexpr int LDS = 2 * LdsSize<N>::value + TW;  // complex elements
+    template <int NS>
+    static constexpr int tw_off() { return P::tw_total - Passes<N, T, NS>::tw_total; }
+};
+
+template <int N, int T, int NS>
+__device__ __forceinline__ void fill_twiddles(double2 *twl, const double2 *__restrict__ tw, int t) {
+    if constexpr (NS < N) {
+        using P = Passes<N, T, NS>;
+        constexpr int R = P::R, S = N / (NS * R), off = FftPlan<N, T>::template tw_off<NS>();
+        if constexpr (NS > 1) {
+            for (int e = t; e < P::tw_here; e += T) {
+                int m;
+                if constexpr (NS <= 256) m = e * S;
+                else m = e < 64 ? e * S : 64 * (e - 64) * S;
+                twl[off + e] = tw[m];
+            }
+        }
+        fill_twiddles<N, T, NS * R>(twl, tw, t);
+    }
+}
+
+// Fill the LDS twiddle tables (caller synchronises before the first transform).
+template <int N, int T>
+__device__ __forceinline__ void fft_init_twiddles(double2 *twl, const double2 *__restrict__ tw) {
+    fill_twiddles<N, T, 1>(twl, tw, threadIdx.x);
+}
+
+// One pass: butterflies j = t, t + T, ...; reads `src` (layout of the writer with stride
+// IN_NS) or registers `io` (FROM_REG), writes `dst` with layout lay<NS> then a barrier, or
+// leaves the result in `io` (TO_REG, no barrier).
+template <int N, int T, int NS, int IN_NS, bool INV, bool FROM_REG, bool TO_REG>
+__device__ __forceinline__ void fft_pass(const double2 *src, double2 *dst, const double2 *twl, int t,
+                                         double2 (&io)[PassRadix<N, T, NS>::value]) {
+    constexpr int R = PassRadix<N, T, NS>::value;
+    constexpr int NB = N / R;
+    constexpr int PER = (NB + T - 1) / T;
+    static_assert(!(FROM_REG || TO_REG) || (NB == T), "register I/O needs one butterfly per thread");
     double2 v[PER][R];
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
@@ -88,11 +164,17 @@ __device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__res
         if (NB % T == 0 || j < NB) {
             const int k = j % NS;
 #pragma unroll
-            for (int r = 0; r < R; ++r) v[p][r] = buf[lpad(j + r * NB)];
+            for (int r = 0; r < R; ++r) {
+                if constexpr (FROM_REG) v[p][r] = io[r];
+                else v[p][r] = src[lay<IN_NS>(j + r * NB)];
+            }
             if constexpr (NS > 1) {
-                // W^(r k) by repeated multiplication of one table twiddle W^k (error <= R eps)
-                double2 w = tw[k * (N / (NS * R))];
+                constexpr int off = FftPlan<N, T>::template tw_off<NS>();
+                double2 w;
+                if constexpr (NS <= 256) w = twl[off + k];
+                else w = cmul(twl[off + (k & 63)], twl[off + 64 + (k >> 6)]);
                 if (INV) w.y = -w.y;
+                // W^(r k) by repeated multiplication (error <= R eps)
                 double2 wr = w;
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
@@ -103,30 +185,42 @@ __device__ __forceinline__ void stockham_pass(double2 *buf, const double2 *__res
             dftR<R, INV>(v[p]);
         }
     }
-    __syncthreads();
+    if constexpr (TO_REG) {
 #pragma unroll
-    for (int p = 0; p < PER; ++p) {
-        const int j = t + p * T;
-        if (NB % T == 0 || j < NB) {
-            const int k = j % NS;
-            const int base = (j / NS) * NS * R + k;
+        for (int r = 0; r < R; ++r) io[r] = v[0][r];
+    } else {
 #pragma unroll
-            for (int r = 0; r < R; ++r) buf[lpad(base + r * NS)] = v[p][r];
+        for (int p = 0; p < PER; ++p) {
+            const int j = t + p * T;
+            if (NB % T == 0 || j < NB) {
+                const int k = j % NS;
+                const int base = (j / NS) * NS * R + k;
+#pragma unroll
+                for (int r = 0; r < R; ++r) dst[lay<NS>(base + r * NS)] = v[p][r];
+            }
         }
+        __syncthreads();
     }
-    __syncthreads();
 }
 
-template <int N, int T, int NS, bool INV>
-__device__ __forceinline__ void fft_passes(double2 *buf, const double2 *__restrict__ tw, int t) {
+// Passes NS .. end, ping-ponging src -> dst.  LAST_REG: the final pass leaves its output in
+// `io` (element t + r*T).  Returns nothing; which buffer holds the result is FftRun::final.
+template <int N, int T, int NS, int IN_NS, bool INV, bool LAST_REG>
+__device__ __forceinline__ void fft_run(double2 *src, double2 *dst, const double2 *twl, int t,
+                                        double2 (&io)[FftPlan<N, T>::R_LAST]) {
     if constexpr (NS < N) {
         constexpr int R = PassRadix<N, T, NS>::value;
-        stockham_pass<N, T, R, NS, INV>(buf, tw, t);
-        fft_passes<N, T, NS * R, INV>(buf, tw, t);
+        if constexpr (LAST_REG && NS * R >= N) {
+            fft_pass<N, T, NS, IN_NS, INV, false, true>(src, dst, twl, t, io);
+        } else {
+            double2 dummy[R];
+            fft_pass<N, T, NS, IN_NS, INV, false, false>(src, dst, twl, t, dummy);
+            fft_run<N, T, NS * R, NS, INV, LAST_REG>(dst, src, twl, t, io);
+        }
     }
 }
 
-// threadIdx.x laundered through an opaque move: the FFT's LDS addresses and twiddle indices
+// thread index laundered through an opaque move: the FFT's LDS addresses and twiddle indices
 // are row-invariant, and without this the compiler hoists all of them (several passes' worth)
 // out of the caller's row loop and keeps them live in VGPRs
 __device__ __forceinline__ int opaque_tid() {
@@ -135,11 +229,37 @@ __device__ __forceinline__ int opaque_tid() {
     return t;
 }
 
-// Unnormalised DFT of buf[lpad(0..N)) in place (natural order in and out).  Caller must have
-// synchronised after writing buf; returns after a barrier.
+// Forward/inverse transform whose input row is in b0 (identity layout, written by the caller
+// and synchronised).  Result: registers `io` (element t + r*T) when OUT_REG, else the buffer
+// b0 or b1 named by result_in_b1 with layout lay<LAST_NS>.
+template <int N, int T, bool INV, bool OUT_REG>
+struct FftFromLds {
+    using Plan = FftPlan<N, T>;
+    // passes that write a buffer: all, or all but the last
+    static constexpr int WRITES = Plan::NPASS - (OUT_REG ? 1 : 0);
+    static constexpr bool result_in_b1 = (WRITES % 2) == 1;
+    // buffer read after the last barrier (by the last pass when OUT_REG, else by the caller)
+    static constexpr bool b0_read_late = OUT_REG ? (WRITES % 2 == 0) : !result_in_b1;
+    __device__ static __forceinline__ void run(double2 *b0, double2 *b1, const double2 *twl,
+                                               double2 (&io)[Plan::R_LAST]) {
+        fft_run<N, T, 1, 0, INV, OUT_REG>(b0, b1, twl, opaque_tid(), io);
+    }
+};
+
+// Transform whose input is in registers `in` (element t + r*T, needs Plan::REG_IN).  Result
+// in b0 or b1 (result_in_b1) with layout lay<LAST_NS>, synchronised.
 template <int N, int T, bool INV>
-__device__ __forceinline__ void fft_lds(double2 *buf, const double2 *__restrict__ tw) {
-    fft_passes<N, T, 1, INV>(buf, tw, opaque_tid());
-}
+struct FftFromReg {
+    using Plan = FftPlan<N, T>;
+    static constexpr bool result_in_b1 = (Plan::NPASS % 2) == 0;
+    static constexpr bool b0_read_late = !result_in_b1;
+    __device__ static __forceinline__ void run(double2 (&in)[Plan::R0], double2 *b0, double2 *b1,
+                                               const double2 *twl) {
+        const int t = opaque_tid();
+        fft_pass<N, T, 1, 0, INV, true, false>(nullptr, b0, twl, t, in);
+        double2 dummy[Plan::R_LAST];
+        fft_run<N, T, Plan::R0, 1, INV, false>(b0, b1, twl, t, dummy);
+    }
+};
 
 }  // namespace qg

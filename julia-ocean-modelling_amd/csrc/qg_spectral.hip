@@ -35,7 +35,16 @@ template <int N>
 __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a) {
     using G = Geo<N>;
     constexpr int T = G::T, KQ = G::KQ, EP = G::EP, NH = N / 2;
-    extern __shared__ double2 buf[];
+    using Plan = FftPlan<N, T>;
+    using FwdReg = FftFromReg<N, T, false>;
+    using FwdLds = FftFromLds<N, T, false, false>;
+    constexpr bool RES_B1 = Plan::REG_IN ? FwdReg::result_in_b1 : FwdLds::result_in_b1;
+    constexpr bool B0_LATE = Plan::REG_IN ? FwdReg::b0_read_late : FwdLds::b0_read_late;
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *b1 = lds + LdsSize<N>::value, *twl = lds + 2 * LdsSize<N>::value;
+    const double2 *Zb = RES_B1 ? b1 : b0;
+    fft_init_twiddles<N, T>(twl, a.tw);
+    __syncthreads();
     const int t = threadIdx.x, c = blockIdx.x;
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
@@ -71,48 +80,60 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     load_row(e);
     for (int j = e; j >= s0; --j) {
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
+        if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
+            double2 in[Plan::R0];
 #pragma unroll
-        for (int p = 0; p < EP; ++p) {
-            const int i = t + p * T;
-            if (N % T == 0 || i < N) buf[lpad(i)] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
+            for (int p = 0; p < EP; ++p) in[p] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
+            if (j > s0) load_row(j - 1);
+            FwdReg::run(in, b0, b1, twl);
+        } else {
+#pragma unroll
+            for (int p = 0; p < EP; ++p) {
+                const int i = t + p * T;
+                if (N % T == 0 || i < N) b0[i] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
+            }
+            if (j > s0) load_row(j - 1);
+            __syncthreads();
+            double2 unused[Plan::R_LAST];
+            FwdLds::run(b0, b1, twl, unused);
         }
-        if (j > s0) load_row(j - 1);
-        __syncthreads();
-        fft_lds<N, T, false>(buf, a.tw);
         double2 *Urow = a.U + (size_t)j * 2 * KS;
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
             if (NH % T == 0 || k < NH) {
-                const double2 Zk = buf[lpad(k)];
+                const double2 Zk = Zb[lay<Plan::LAST_NS>(k)];
                 if (k == 0) {  // the two real lines k = 0 and k = N/2
-                    const double2 Zn = buf[lpad(NH)];
+                    const double2 Zn = Zb[lay<Plan::LAST_NS>(NH)];
                     dc += Zk.x;
                     hline[j] = Zk.x;
                     const double2 B[2] = {make_double2(Zk.x, Zn.x), make_double2(Zk.y, Zn.y)};
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const Coef *c0 = a.coef + s * KS, *cN = a.coef + s * KS + NH;
-                        u[q][s] = make_double2(c0->cs * B[s].x + c0->r * u[q][s].x, cN->cs * B[s].y + cN->r * u[q][s].y);
+                        const int o0 = s * KS, oN = s * KS + NH;
+                        const double2 r0 = a.crr[o0], rN = a.crr[oN];
+                        u[q][s] = make_double2(a.ccs[o0] * B[s].x + r0.x * u[q][s].x,
+                                               a.ccs[oN] * B[s].y + rN.x * u[q][s].y);
                         Urow[s * KS] = make_double2(u[q][s].x, 0);
                         Urow[s * KS + NH] = make_double2(u[q][s].y, 0);
-                        bw[q][s] = make_double2(bw[q][s].x * c0->rinv + u[q][s].x, bw[q][s].y * cN->rinv + u[q][s].y);
+                        bw[q][s] = make_double2(bw[q][s].x * r0.y + u[q][s].x, bw[q][s].y * rN.y + u[q][s].y);
                     }
                 } else {
-                    const double2 Zm = buf[lpad(N - k)];
+                    const double2 Zm = Zb[lay<Plan::LAST_NS>(N - k)];
                     const double2 B[2] = {make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5),
                                           make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5)};
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const Coef *cf = a.coef + s * KS + k;
-                        u[q][s] = cfma(cf->r, u[q][s], cscale(B[s], cf->cs));
+                        const int o = s * KS + k;
+                        const double2 rr = a.crr[o];
+                        u[q][s] = cfma(rr.x, u[q][s], cscale(B[s], a.ccs[o]));
                         Urow[s * KS + k] = u[q][s];
-                        bw[q][s] = cfma(cf->rinv, bw[q][s], u[q][s]);
+                        bw[q][s] = cfma(rr.y, bw[q][s], u[q][s]);
                     }
                 }
             }
         }
-        __syncthreads();
+        if constexpr (B0_LATE) __syncthreads();  // the next row's first pass overwrites b0
     }
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
@@ -138,22 +159,27 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 }
 
 // ------------------------------------------------------------------------------------
-// carry: segment-parallel chunk scans.  Lanes = 64 consecutive k of one system, waves =
-// contiguous segments of chunks.  Zero carries at the rank boundaries (cross-rank and
-// periodic closure are applied by spec_pin / spec_passB).
+// carry: segment-parallel chunk scans.  A workgroup owns CARRY_KB consecutive k of one
+// system; each wave's 64 lanes are CARRY_KB k x (64 / CARRY_KB) chunk segments, so the
+// workgroup runs CARRY_SEG segments per k (short serial chains, ~260 workgroups at M = 4096).
+// Zero carries at the rank boundaries (cross-rank and periodic closure are applied by
+// spec_pin / spec_passB).
 //   v_c = ULS_c + q v_{c+1}, v_Nc = 0      UIN_c = v_{c+1},  AU = v_0
 //   w_c = (WLS_c + gam UIN_c) + q w_{c-1}   WIN_c = w_{c-1},  AW = w_{Nc-1}
 // ------------------------------------------------------------------------------------
+constexpr int CARRY_KB = 16;
+constexpr int CARRY_SEG = CARRY_WAVES * (64 / CARRY_KB);
+
 __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
-    __shared__ double2 agg[CARRY_WAVES][64];
-    __shared__ double qlen_s[CARRY_WAVES][64];
+    __shared__ double2 agg[CARRY_SEG][CARRY_KB];
+    __shared__ double qlen_s[CARRY_SEG][CARRY_KB];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    constexpr int W = CARRY_WAVES;
-    const int k = blockIdx.x * 64 + lane, s = blockIdx.y;
+    const int kk = lane % CARRY_KB, seg = wv * (64 / CARRY_KB) + lane / CARRY_KB;
+    const int k = blockIdx.x * CARRY_KB + kk, s = blockIdx.y;
     const bool ok = k < a.KH;
     const int KS = a.KS, Nc = a.Nc;
-    const int SL = (Nc + W - 1) / W;
-    const int c0 = min(wv * SL, Nc), c1 = min(c0 + SL, Nc);
+    const int SL = (Nc + CARRY_SEG - 1) / CARRY_SEG;
+    const int c0 = min(seg * SL, Nc), c1 = min(c0 + SL, Nc);
     double q = 0, gam = 0;
     if (ok) {
         q = a.coef[s * KS + k].q;
@@ -164,22 +190,25 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
 
     double2 v = make_double2(0, 0);
     double qlen = 1;
-    if (ok)
+    if (ok) {
+#pragma unroll 4
         for (int c = c1 - 1; c >= c0; --c) {
             v = cfma(q, v, at(a.ULS, c));
             qlen *= q;
         }
-    agg[wv][lane] = v;
-    qlen_s[wv][lane] = qlen;
+    }
+    agg[seg][kk] = v;
+    qlen_s[seg][kk] = qlen;
     __syncthreads();
     double2 vin = make_double2(0, 0);
-    for (int g = W - 1; g > wv; --g) vin = cfma(qlen_s[g][lane], vin, agg[g][lane]);
+    for (int g = CARRY_SEG - 1; g > seg; --g) vin = cfma(qlen_s[g][kk], vin, agg[g][kk]);
     __syncthreads();
 
     double2 bsum = make_double2(0, 0);
     double wq = 1;
     v = vin;
-    if (ok)
+    if (ok) {
+#pragma unroll 4
         for (int c = c1 - 1; c >= c0; --c) {
             put(a.UIN, c, v);
             const double2 wt = cfma(gam, v, at(a.WLS, c));
@@ -187,26 +216,29 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
             wq *= q;
             v = cfma(q, v, at(a.ULS, c));
         }
-    if (wv == 0 && ok) {
+    }
+    if (seg == 0 && ok) {
         reinterpret_cast<double2 *>(a.rec + rec_AU(KS))[s * KS + k] = v;
         if (s == 0) {
             reinterpret_cast<double2 *>(a.rec + rec_ULS0(KS))[k] = at(a.ULS, 0);
             reinterpret_cast<double2 *>(a.rec + rec_UIN0(KS))[k] = at(a.UIN, 0);
         }
     }
-    agg[wv][lane] = bsum;
+    agg[seg][kk] = bsum;
     __syncthreads();
     double2 win = make_double2(0, 0);
-    for (int g = 0; g < wv; ++g) win = cfma(qlen_s[g][lane], win, agg[g][lane]);
+    for (int g = 0; g < seg; ++g) win = cfma(qlen_s[g][kk], win, agg[g][kk]);
 
     double2 w = win;
-    if (ok)
+    if (ok) {
+#pragma unroll 4
         for (int c = c0; c < c1; ++c) {
             put(a.WIN, c, w);
             const double2 wt = cfma(gam, at(a.UIN, c), at(a.WLS, c));
             w = cfma(q, w, wt);
         }
-    if (wv == W - 1 && ok) reinterpret_cast<double2 *>(a.rec + rec_AW(KS))[s * KS + k] = w;
+    }
+    if (seg == CARRY_SEG - 1 && ok) reinterpret_cast<double2 *>(a.rec + rec_AW(KS))[s * KS + k] = w;
     if (blockIdx.x == 0 && s == 0 && threadIdx.x == 0) {
         double d = 0;
         for (int c = 0; c < Nc; ++c) d += a.dcpart[c];
@@ -219,32 +251,38 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
 // workgroup; every rank runs it redundantly on the gathered records (same order -> same
 // bits everywhere).
 // ------------------------------------------------------------------------------------
-__device__ double block_sum(double v, double *red) {  // fixed-order tree reduction
-    const int t = threadIdx.x;
-    red[t] = v;
+// Block-wide reductions of the pin kernel: wave64 shuffles, then the 16 wave totals combined
+// by every thread in a fixed order (same bits on every rank), two barriers per call.
+constexpr int PIN_WAVES = PIN_THREADS / 64;
+
+__device__ double block_sum(double v, double *red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[w] = v;
     __syncthreads();
-    for (int o = PIN_THREADS / 2; o > 0; o >>= 1) {
-        if (t < o) red[t] += red[t + o];
-        __syncthreads();
-    }
-    const double r = red[0];
+    double r = 0;
+    for (int g = 0; g < PIN_WAVES; ++g) r += red[g];
     __syncthreads();
     return r;
 }
 
-__device__ double block_exscan(double v, double *red) {  // exclusive prefix sum, fixed order
-    const int t = threadIdx.x;
-    red[t] = v;
-    __syncthreads();
-    for (int o = 1; o < PIN_THREADS; o <<= 1) {
-        const double add = t >= o ? red[t - o] : 0.0;
-        __syncthreads();
-        red[t] += add;
-        __syncthreads();
+__device__ double block_exscan(double v, double *red) {  // exclusive prefix sum in thread order
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
     }
-    const double incl = red[t];
+    if (lane == 63) red[w] = incl;
     __syncthreads();
-    return incl - v;
+    double base = 0;
+    for (int g = 0; g < w; ++g) base += red[g];
+    __syncthreads();
+    double ex = __shfl_up(incl, 1, 64);
+    if (lane == 0) ex = 0;
+    return base + ex;
 }
 
 __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
@@ -373,7 +411,13 @@ template <int N>
 __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a) {
     using G = Geo<N>;
     constexpr int T = G::T, KQ = G::KQ, EP = G::EP, NH = N / 2;
-    extern __shared__ double2 buf[];
+    using Plan = FftPlan<N, T>;
+    using Inv = FftFromLds<N, T, true, Plan::REG_OUT>;
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *b1 = lds + LdsSize<N>::value, *twl = lds + 2 * LdsSize<N>::value;
+    const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
+    fft_init_twiddles<N, T>(twl, a.tw);
+    __syncthreads();
     const int t = threadIdx.x, c = blockIdx.x;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     const int KS = a.KS;
@@ -440,38 +484,41 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                     double x0[2], xN[2];
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const Coef *c0 = a.coef + s * KS, *cN = a.coef + s * KS + NH;
+                        const int o0 = s * KS, oN = s * KS + NH;
                         double ul0 = ucur[q][s].x, ulN = ucur[q][s].y;
                         if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
-                            ul0 += c0->cs * delta;
-                            ulN += cN->cs * delta;
+                            ul0 += a.ccs[o0] * delta;
+                            ulN += a.ccs[oN] * delta;
                         }
-                        const double wx = c0->r * w[q][s].x + (ul0 + cu[q][s].x);
-                        const double wy = cN->r * w[q][s].y + (ulN + cu[q][s].y);
+                        const double2 r0 = a.crr[o0], rN = a.crr[oN];
+                        const double wx = r0.x * w[q][s].x + (ul0 + cu[q][s].x);
+                        const double wy = rN.x * w[q][s].y + (ulN + cu[q][s].y);
                         w[q][s] = make_double2(wx, wy);
-                        cu[q][s] = make_double2(cu[q][s].x * c0->rinv, cu[q][s].y * cN->rinv);
+                        cu[q][s] = make_double2(cu[q][s].x * r0.y, cu[q][s].y * rN.y);
                         x0[s] = (s == 0 && sing) ? a.line[j] : wx;
                         xN[s] = wy;
                     }
-                    buf[lpad(0)] = make_double2(x0[0], x0[1]);
-                    buf[lpad(NH)] = make_double2(xN[0], xN[1]);
+                    b0[0] = make_double2(x0[0], x0[1]);
+                    b0[NH] = make_double2(xN[0], xN[1]);
                 } else {
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const Coef *cf = a.coef + s * KS + k;
+                        const int o = s * KS + k;
                         double2 ul = ucur[q][s];
-                        if (s == 0 && inject && j == 0) ul.x += cf->cs * delta;
-                        w[q][s] = cfma(cf->r, w[q][s], cadd(ul, cu[q][s]));
-                        cu[q][s] = cscale(cu[q][s], cf->rinv);
+                        if (s == 0 && inject && j == 0) ul.x += a.ccs[o] * delta;
+                        const double2 rr = a.crr[o];
+                        w[q][s] = cfma(rr.x, w[q][s], cadd(ul, cu[q][s]));
+                        cu[q][s] = cscale(cu[q][s], rr.y);
                         X[s] = w[q][s];
                     }
-                    buf[lpad(k)] = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
-                    buf[lpad(N - k)] = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
+                    b0[k] = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
+                    b0[N - k] = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
                 }
             }
         }
         __syncthreads();
-        fft_lds<N, T, true>(buf, a.tw);
+        double2 xo[Plan::R_LAST];  // last FFT pass output in registers: element t + r*T
+        Inv::run(b0, b1, twl, xo);
         double *row1 = a.out1 + (size_t)(j + 1) * ld;
         double *grow1 = ghost_row_target(a.out1, ld, Pl, j, a.write_ghost_rows);
         double *row2 = a.out2 ? a.out2 + (size_t)(j + 1) * ld : nullptr;
@@ -480,13 +527,15 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         for (int p = 0; p < EP; ++p) {
             const int i = t + p * T;
             if (N % T == 0 || i < N) {
-                const double2 z = buf[lpad(i)];
+                double2 z;
+                if constexpr (Plan::REG_OUT) z = xo[p];
+                else z = Xb[lay<Plan::LAST_NS>(i)];
                 const double x1 = z.x - pin, x2 = z.y;
                 store_row_with_ghosts(row1, grow1, N, i, a.pin_out[0] * x1 + a.pin_out[1] * x2);
                 if (row2) store_row_with_ghosts(row2, grow2, N, i, a.pin_out[2] * x1 + a.pin_out[3] * x2);
             }
         }
-        __syncthreads();
+        if constexpr (Inv::b0_read_late) __syncthreads();  // the next row's recurrence writes b0
     }
 }
 
@@ -495,7 +544,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 // ------------------------------------------------------------------------------------
 template <int N>
 static int launch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
-    const size_t lds = sizeof(double2) * LdsSize<N>::value;
+    const size_t lds = sizeof(double2) * FftPlan<N, Geo<N>::T>::LDS;
     if (passB) {
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         spec_passB<N><<<a.Nc, Geo<N>::T, lds, s>>>(a);
@@ -598,6 +647,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     // ---- device memory ---------------------------------------------------------------
     const size_t n_tw = align_up(sizeof(double2) * M);
     const size_t n_coef = align_up(sizeof(Coef) * coef.size());
+    const size_t n_hot = align_up(sizeof(double) * 6 * (size_t)KS);
     const size_t n_U = align_up(sizeof(double2) * (size_t)P * 2 * KS);
     const size_t n_S = align_up(sizeof(double2) * (size_t)a.Nc * 2 * KS);
     const size_t n_dc = align_up(sizeof(double) * a.Nc);
@@ -608,7 +658,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const size_t n_line = align_up(sizeof(double) * P);
     const size_t n_scal = align_up(sizeof(double) * 8);
     const size_t n_work = align_up(sizeof(double) * P_total);
-    bytes_ = n_tw + n_coef + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + n_line + n_scal + n_work;
+    bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + n_line + n_scal + n_work;
     if (hipMalloc(&mem_, bytes_) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -617,6 +667,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     auto take = [&](size_t n) { char *r = p; p += n; return r; };
     double2 *d_tw = (double2 *)take(n_tw);
     Coef *d_coef = (Coef *)take(n_coef);
+    double *d_hot = (double *)take(n_hot);
     a.U = (double2 *)take(n_U);
     a.ULS = (double2 *)take(n_S);
     a.WLS = (double2 *)take(n_S);
@@ -635,6 +686,17 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.coef = d_coef;
     QG_HIP(hipMemcpy(d_tw, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice));
     QG_HIP(hipMemcpy(d_coef, coef.data(), sizeof(Coef) * coef.size(), hipMemcpyHostToDevice));
+    {
+        std::vector<double> hot(6 * (size_t)KS);  // [2][KS] (r, 1/r) pairs, then [2][KS] cs
+        for (size_t i = 0; i < 2 * (size_t)KS; ++i) {
+            hot[2 * i] = coef[i].r;
+            hot[2 * i + 1] = coef[i].rinv;
+            hot[4 * KS + i] = coef[i].cs;
+        }
+        QG_HIP(hipMemcpy(d_hot, hot.data(), sizeof(double) * hot.size(), hipMemcpyHostToDevice));
+        a.crr = reinterpret_cast<const double2 *>(d_hot);
+        a.ccs = d_hot + 4 * KS;
+    }
     QG_HIP(hipMemset(a.rec, 0, n_rec));
     QG_HIP(hipMemset(a.scal, 0, n_scal));
     QG_HIP(hipMemset(a.line, 0, n_line));
@@ -655,7 +717,7 @@ int SpectralSolver::solve(const double *in1, const double *in2, double *out1, do
     a.out2 = out2;
     a.write_ghost_rows = write_ghost_rows;
     QG_CHECK(dispatch_pass(false, a, s));
-    spec_carry<<<dim3((unsigned)((a.KH + 63) / 64), 2), 64 * CARRY_WAVES, 0, s>>>(a);
+    spec_carry<<<dim3((unsigned)((a.KH + CARRY_KB - 1) / CARRY_KB), 2), 64 * CARRY_WAVES, 0, s>>>(a);
     QG_LAUNCH_CHECK();
     if (a.nranks > 1) {
         if (!gather) return QG_ERR_RCCL;

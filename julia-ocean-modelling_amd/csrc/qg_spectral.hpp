@@ -44,6 +44,8 @@ struct SpecArgs {
     double *out1, *out2;
     const double2 *tw;        // M twiddles
     const Coef *coef;         // [2][KS]
+    const double2 *crr;       // [2][KS] (r, 1/r) of coef, unit-stride for the row loops
+    const double *ccs;        // [2][KS] cs of coef
     double2 *U;               // [P][2][KS]
     double2 *ULS, *WLS;       // [Nc][2][KS]
     double2 *UIN, *WIN;       // [Nc][2][KS]
