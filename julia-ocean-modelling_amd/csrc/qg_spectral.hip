@@ -9,7 +9,8 @@
 namespace qg {
 
 constexpr int CARRY_WAVES = 8;
-constexpr int PIN_THREADS = 1024;
+constexpr int PIN_THREADS = 256;
+__host__ __device__ inline int pin_kblocks(int KH) { return (2 * KH + PIN_THREADS - 1) / PIN_THREADS; }
 
 template <int N>
 struct Geo {
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         }
     const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
     double dc = 0;
-    double *hline = a.rec + rec_HLINE(KS);
+    double *hline = a.hline;
     // register prefetch: row j-1 is loaded while row j is transformed (the barriers only wait
     // for LDS traffic, so the global loads stay in flight across the FFT)
     double pf1[EP], pf2[EP];
@@ -158,6 +159,102 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     if (t == 0) a.dcpart[c] = dc;
 }
 
+// Block-wide reductions: wave64 shuffles, then the wave totals combined by every thread in a
+// fixed order (same bits on every rank), two barriers per call.  red: >= NT/64 doubles.
+template <int NT>
+__device__ double block_sum(double v, double *red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double r = 0;
+    for (int g = 0; g < NT / 64; ++g) r += red[g];
+    __syncthreads();
+    return r;
+}
+
+template <int NT>
+__device__ double block_exscan(double v, double *red) {  // exclusive prefix sum in thread order
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) red[w] = incl;
+    __syncthreads();
+    double base = 0;
+    for (int g = 0; g < w; ++g) base += red[g];
+    __syncthreads();
+    double ex = __shfl_up(incl, 1, 64);
+    if (lane == 0) ex = 0;
+    return base + ex;
+}
+
+// The local part of the singular k = 0 Poisson line (one workgroup of NT threads).  With h_j
+// the rank's line, S_j = sum_{i<=j} h_i and m_loc = mean S, it writes
+//   line_j = dx^2/M * sum_{i<j} (S_i - m_loc)
+// and records H = S_{P-1}, Q = sum S.  The global line (spec_pin) is this plus an affine
+// correction in j; for one rank the correction is exactly zero.  Tiled block scans: tiles of
+// NT * LINE_PER values staged in LDS with coalesced accesses, LINE_PER consecutive values per
+// thread, running carries between tiles; the second sweep recomputes S instead of storing it.
+constexpr int LINE_PER = 8;
+template <int NT>
+__device__ void local_line(const SpecArgs &a, double *red, double *tile) {
+    constexpr int TILE = NT * LINE_PER;
+    const int t = threadIdx.x, n = (int)a.P;
+    auto tp = [](int x) { return x + (x >> 4); };  // pad: conflict-free strided b64 reads
+    auto stage_h = [&](int j0) {
+        for (int u = t; u < TILE; u += NT) tile[tp(u)] = j0 + u < n ? a.hline[j0 + u] : 0.0;
+        __syncthreads();
+    };
+    // scan of this thread's LINE_PER staged values (after f(value, j)) joined across the
+    // workgroup and offset by `carry`; inclusive or exclusive; returns the tile total
+    auto scan_tile = [&](double carry, bool excl, auto f, int j0) {
+        double v[LINE_PER], acc = 0;
+#pragma unroll
+        for (int u = 0; u < LINE_PER; ++u) {
+            const int x = t * LINE_PER + u;
+            const double d = f(tile[tp(x)], j0 + x);
+            v[u] = excl ? acc : acc + d;
+            acc += d;
+        }
+        const double off = carry + block_exscan<NT>(acc, red);
+#pragma unroll
+        for (int u = 0; u < LINE_PER; ++u) tile[tp(t * LINE_PER + u)] = off + v[u];
+        return block_sum<NT>(acc, red);  // ends with a barrier: the scanned tile is visible
+    };
+    auto ident = [](double x, int) { return x; };
+    double carryS = 0, q = 0;
+    for (int j0 = 0; j0 < n; j0 += TILE) {  // sweep 1: S, its total H and its sum Q
+        stage_h(j0);
+        carryS += scan_tile(carryS, false, ident, j0);
+        for (int u = t; u < TILE; u += NT)
+            if (j0 + u < n) q += tile[tp(u)];
+        __syncthreads();
+    }
+    const double Q = block_sum<NT>(q, red), H = carryS;
+    const double mloc = Q / (double)n;
+    const double scale = (a.dx * a.dx) / (double)a.M;
+    carryS = 0;
+    double carryX = 0;
+    auto dev = [&](double S, int j) { return j < n ? S - mloc : 0.0; };
+    for (int j0 = 0; j0 < n; j0 += TILE) {  // sweep 2: S again, then X = exclusive scan of S - m
+        stage_h(j0);
+        carryS += scan_tile(carryS, false, ident, j0);
+        carryX += scan_tile(carryX, true, dev, j0);
+        for (int u = t; u < TILE; u += NT)
+            if (j0 + u < n) a.line[j0 + u] = scale * tile[tp(u)];
+        __syncthreads();
+    }
+    if (t == 0) {
+        a.rec[rec_DSUM(a.KS) + 1] = H;
+        a.rec[rec_DSUM(a.KS) + 2] = Q;
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // carry: segment-parallel chunk scans.  A workgroup owns CARRY_KB consecutive k of one
 // system; each wave's 64 lanes are CARRY_KB k x (64 / CARRY_KB) chunk segments, so the
@@ -173,6 +270,14 @@ constexpr int CARRY_SEG = CARRY_WAVES * (64 / CARRY_KB);
 __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
     __shared__ double2 agg[CARRY_SEG][CARRY_KB];
     __shared__ double qlen_s[CARRY_SEG][CARRY_KB];
+    if ((int)blockIdx.x == (a.KH + CARRY_KB - 1) / CARRY_KB) {  // the extra column
+        if (blockIdx.y == 0 && a.pinned0) {
+            __shared__ double red[CARRY_WAVES];
+            __shared__ double tile[64 * CARRY_WAVES * LINE_PER * 17 / 16];
+            local_line<64 * CARRY_WAVES>(a, red, tile);
+        }
+        return;
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int kk = lane % CARRY_KB, seg = wv * (64 / CARRY_KB) + lane / CARRY_KB;
     const int k = blockIdx.x * CARRY_KB + kk, s = blockIdx.y;
@@ -251,40 +356,6 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
 // workgroup; every rank runs it redundantly on the gathered records (same order -> same
 // bits everywhere).
 // ------------------------------------------------------------------------------------
-// Block-wide reductions of the pin kernel: wave64 shuffles, then the 16 wave totals combined
-// by every thread in a fixed order (same bits on every rank), two barriers per call.
-constexpr int PIN_WAVES = PIN_THREADS / 64;
-
-__device__ double block_sum(double v, double *red) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    double r = 0;
-    for (int g = 0; g < PIN_WAVES; ++g) r += red[g];
-    __syncthreads();
-    return r;
-}
-
-__device__ double block_exscan(double v, double *red) {  // exclusive prefix sum in thread order
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double incl = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const double y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) red[w] = incl;
-    __syncthreads();
-    double base = 0;
-    for (int g = 0; g < w; ++g) base += red[g];
-    __syncthreads();
-    double ex = __shfl_up(incl, 1, 64);
-    if (lane == 0) ex = 0;
-    return base + ex;
-}
-
 __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
     __shared__ double red[PIN_THREADS];
     const int t = threadIdx.x;
@@ -299,93 +370,86 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
         delta = -delta;
     }
 
-    double pin_part = 0;
-    for (int idx = t; idx < 2 * KH; idx += PIN_THREADS) {
+    {
+        double pin_part = 0;
+        const int idx = blockIdx.x * PIN_THREADS + t;
         const int s = idx / KH, k = idx - s * KH;
-        const Coef cf = a.coef[s * KS + k];
-        double2 *Ue = a.EXT + (size_t)s * KS + k;
-        double2 *We = a.EXT + (size_t)(2 + s) * KS + k;
-        if (s == 0 && a.pinned0 && k == 0) {
-            *Ue = make_double2(0, 0);
-            *We = make_double2(0, 0);
-            continue;
-        }
-        const bool dl = (s == 0 && a.pinned0);
-        const double rPl1 = exp((double)(Pl - 1) * cf.lr);
-        auto AU = [&](int g) {
-            double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AU(KS))[s * KS + k];
-            if (dl && g == 0) v.x += cf.cs * delta;
-            return v;
-        };
-        auto AW = [&](int g) {
-            double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AW(KS))[s * KS + k];
-            if (dl && g == 0) v.x += rPl1 * (cf.cs * delta);
-            return v;
-        };
-        auto Uext = [&](int g) {  // u_true at the start of rank g+1 (ring)
-            double2 acc = make_double2(0, 0);
-            for (int m = G - 1; m >= 0; --m) acc = cfma(cf.rP, acc, AU((g + 1 + m) % G));
-            return cscale(acc, cf.inv1mrPt);
-        };
-        auto Wext = [&](int g) {  // w_true at the end of rank g-1 (ring)
-            double2 acc = make_double2(0, 0);
-            for (int m = G - 1; m >= 0; --m) {
-                const int gg = ((g - 1 - m) % G + G) % G;
-                acc = cfma(cf.rP, acc, cfma(cf.gamP, Uext(gg), AW(gg)));
+        if (idx < 2 * KH) {
+            double2 *Ue = a.EXT + (size_t)s * KS + k;
+            double2 *We = a.EXT + (size_t)(2 + s) * KS + k;
+            if (s == 0 && a.pinned0 && k == 0) {
+                *Ue = make_double2(0, 0);
+                *We = make_double2(0, 0);
+            } else {
+                const Coef cf = a.coef[s * KS + k];
+                const bool dl = (s == 0 && a.pinned0);
+                const double rPl1 = exp((double)(Pl - 1) * cf.lr);
+                auto AU = [&](int g) {
+                    double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AU(KS))[s * KS + k];
+                    if (dl && g == 0) v.x += cf.cs * delta;
+                    return v;
+                };
+                auto AW = [&](int g) {
+                    double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AW(KS))[s * KS + k];
+                    if (dl && g == 0) v.x += rPl1 * (cf.cs * delta);
+                    return v;
+                };
+                auto Uext = [&](int g) {  // u_true at the start of rank g+1 (ring)
+                    double2 acc = make_double2(0, 0);
+                    for (int m = G - 1; m >= 0; --m) acc = cfma(cf.rP, acc, AU((g + 1 + m) % G));
+                    return cscale(acc, cf.inv1mrPt);
+                };
+                auto Wext = [&](int g) {  // w_true at the end of rank g-1 (ring)
+                    double2 acc = make_double2(0, 0);
+                    for (int m = G - 1; m >= 0; --m) {
+                        const int gg = ((g - 1 - m) % G + G) % G;
+                        acc = cfma(cf.rP, acc, cfma(cf.gamP, Uext(gg), AW(gg)));
+                    }
+                    return cscale(acc, cf.inv1mrPt);
+                };
+                const double2 ue = Uext(a.rank), we = Wext(a.rank);
+                *Ue = ue;
+                *We = we;
+                if (dl && k >= 1) {  // pinning value: rank 0, chunk 0, row 0
+                    const double2 ue0 = a.rank == 0 ? ue : Uext(0);
+                    const double2 we0 = a.rank == 0 ? we : Wext(0);
+                    double2 u0 = reinterpret_cast<const double2 *>(rec(0) + rec_ULS0(KS))[k];
+                    u0.x += cf.cs * delta;
+                    const double2 uin0 = cfma(exp((double)(a.Nc - 1) * a.L * cf.lr), ue0,
+                                              reinterpret_cast<const double2 *>(rec(0) + rec_UIN0(KS))[k]);
+                    const double2 w0 = cfma(cf.r, we0, cfma(cf.q, uin0, u0));
+                    const double X = w0.x;
+                    pin_part = (2 * k == a.M) ? X : 2 * X;
+                }
             }
-            return cscale(acc, cf.inv1mrPt);
-        };
-        const double2 ue = Uext(a.rank), we = Wext(a.rank);
-        *Ue = ue;
-        *We = we;
-        if (dl && k >= 1) {  // pinning value: rank 0, chunk 0, row 0
-            const double2 ue0 = a.rank == 0 ? ue : Uext(0);
-            const double2 we0 = a.rank == 0 ? we : Wext(0);
-            double2 u0 = reinterpret_cast<const double2 *>(rec(0) + rec_ULS0(KS))[k];
-            u0.x += cf.cs * delta;
-            const double2 uin0 = cfma(exp((double)(a.Nc - 1) * a.L * cf.lr), ue0,
-                                      reinterpret_cast<const double2 *>(rec(0) + rec_UIN0(KS))[k]);
-            const double2 w0 = cfma(cf.r, we0, cfma(cf.q, uin0, u0));
-            const double X = w0.x;
-            pin_part += (2 * k == a.M) ? X : 2 * X;
+        }
+        const double part = block_sum<PIN_THREADS>(pin_part, red);  // this workgroup's share of the pin
+        if (t == 0) a.pinpart[blockIdx.x] = part;
+        if (blockIdx.x == 0 && t == 0) {
+            a.scal[0] = delta;
+            if (a.pinned0) {  // affine correction of the singular line (see local_line)
+                // S_j = C_g + S_loc_j on rank g, C_g = sum_{g'<g} H_g'; m = global mean of S;
+                // X_j = Xs_g + j (C_g - m + m_loc) + X_loc_j with Xs_g = sum_{g'<g} (P C_g' + Q_g' - P m)
+                const double P = (double)Pl;
+                double C = 0, tot = 0;
+                for (int g = 0; g < G; ++g) {
+                    tot += P * C + rec(g)[rec_DSUM(KS) + 2];
+                    C += rec(g)[rec_DSUM(KS) + 1];
+                }
+                const double m = tot / (double)Pt;
+                double Cr = 0, Xs = 0;
+                for (int g = 0; g < a.rank; ++g) {
+                    Xs += (P * Cr + rec(g)[rec_DSUM(KS) + 2]) - P * m;
+                    Cr += rec(g)[rec_DSUM(KS) + 1];
+                }
+                const double mloc = rec(a.rank)[rec_DSUM(KS) + 2] / P;
+                const double scale = (a.dx * a.dx) / (double)a.M;
+                a.scal[2] = scale * Xs;
+                a.scal[3] = scale * ((Cr - m) + mloc);
+            }
         }
     }
-    const double pin = block_sum(pin_part, red);
 
-    if (a.pinned0) {  // singular k = 0 Poisson line over the global y extent
-        const int64_t n = Pt;
-        const int64_t len = (n + PIN_THREADS - 1) / PIN_THREADS;
-        const int64_t b0 = min((int64_t)t * len, n), b1 = min(b0 + len, n);
-        auto h = [&](int64_t jg) {
-            const int g = (int)(jg / Pl);
-            double v = rec(g)[rec_HLINE(KS) + (jg - (int64_t)g * Pl)];
-            if (jg == 0) v += delta;
-            return v;
-        };
-        double sh = 0;
-        for (int64_t j = b0; j < b1; ++j) sh += h(j);
-        double run = block_exscan(sh, red);
-        double sS = 0;
-        for (int64_t j = b0; j < b1; ++j) {
-            run += h(j);
-            a.work[j] = run;  // S_j (inclusive)
-            sS += run;
-        }
-        const double meanS = block_sum(sS, red) / (double)n;
-        double sD = 0;
-        for (int64_t j = b0; j < b1; ++j) sD += a.work[j] - meanS;
-        double X = block_exscan(sD, red);  // X_j = sum_{i<j} (S_i - meanS)
-        const double scale = (a.dx * a.dx) / (double)a.M;
-        const int64_t lo = (int64_t)a.rank * Pl;
-        for (int64_t j = b0; j < b1; ++j) {
-            if (j >= lo && j < lo + Pl) a.line[j - lo] = scale * X;
-            X += a.work[j] - meanS;
-        }
-    }
-    if (t == 0) {
-        a.scal[0] = delta;
-        a.scal[1] = a.pinned0 ? pin : 0.0;
-    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -422,9 +486,16 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
-    const double delta = a.scal[0], pin = a.scal[1];
+    const double delta = a.scal[0];
+    double pin = 0;  // sum of the pin kernel's per-workgroup parts, fixed order
+    if (a.pinned0) {
+        const int nbk = pin_kblocks(a.KH);
+        for (int b = 0; b < nbk; ++b) pin += a.pinpart[b];
+    }
+    if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     const bool inject = a.pinned0 && a.rank == 0;
     const bool sing = a.pinned0;  // (s = 0, k = 0) is the singular line, served by a.line
+    const double line0 = a.scal[2], line1 = a.scal[3];
 
     // per line: carried term cu = r^(e+1-j) u_in and forward-filter state w.  Slot (0, t = 0)
     // packs the real lines k = 0 (.x) and k = N/2 (.y).
@@ -464,14 +535,21 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             }
         }
     };
+#ifndef QG_PASSB_NO_PREFETCH
     load_u(s0);
+#endif
     for (int j = s0; j <= e; ++j) {
+#ifdef QG_PASSB_NO_PREFETCH
+        load_u(j);
+#endif
         double2 ucur[KQ][2];
 #pragma unroll
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
             for (int s = 0; s < 2; ++s) ucur[q][s] = upf[q][s];
+#ifndef QG_PASSB_NO_PREFETCH
         if (j < e) load_u(j + 1);
+#endif
         // compiler memory barrier: re-read the (L1-resident) coefficients every row instead of
         // hoisting them into registers, which would spill at this occupancy
         asm volatile("" ::: "memory");
@@ -495,7 +573,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                         const double wy = rN.x * w[q][s].y + (ulN + cu[q][s].y);
                         w[q][s] = make_double2(wx, wy);
                         cu[q][s] = make_double2(cu[q][s].x * r0.y, cu[q][s].y * rN.y);
-                        x0[s] = (s == 0 && sing) ? a.line[j] : wx;
+                        x0[s] = (s == 0 && sing) ? (line0 + (double)j * line1) + a.line[j] : wx;
                         xN[s] = wy;
                     }
                     b0[0] = make_double2(x0[0], x0[1]);
@@ -655,10 +733,10 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const size_t n_rec = align_up(sizeof(double) * RS);
     const size_t n_grec = align_up(sizeof(double) * RS * nranks);  // gather target (also 1-rank ring)
     const size_t n_ext = align_up(sizeof(double2) * 4 * KS);
-    const size_t n_line = align_up(sizeof(double) * P);
+    const size_t n_line = align_up(sizeof(double) * P);  // (hline and line)
     const size_t n_scal = align_up(sizeof(double) * 8);
-    const size_t n_work = align_up(sizeof(double) * P_total);
-    bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + n_line + n_scal + n_work;
+    const size_t n_pinpart = align_up(sizeof(double) * (pin_kblocks(a.KH) + 1));
+    bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart;
     if (hipMalloc(&mem_, bytes_) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -680,8 +758,9 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.rec_stride = RS;
     a.EXT = (double2 *)take(n_ext);
     a.line = (double *)take(n_line);
+    a.hline = (double *)take(n_line);
     a.scal = (double *)take(n_scal);
-    a.work = (double *)take(n_work);
+    a.pinpart = (double *)take(n_pinpart);
     a.tw = d_tw;
     a.coef = d_coef;
     QG_HIP(hipMemcpy(d_tw, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice));
@@ -717,7 +796,7 @@ int SpectralSolver::solve(const double *in1, const double *in2, double *out1, do
     a.out2 = out2;
     a.write_ghost_rows = write_ghost_rows;
     QG_CHECK(dispatch_pass(false, a, s));
-    spec_carry<<<dim3((unsigned)((a.KH + CARRY_KB - 1) / CARRY_KB), 2), 64 * CARRY_WAVES, 0, s>>>(a);
+    spec_carry<<<dim3((unsigned)((a.KH + CARRY_KB - 1) / CARRY_KB) + 1, 2), 64 * CARRY_WAVES, 0, s>>>(a);
     QG_LAUNCH_CHECK();
     if (a.nranks > 1) {
         if (!gather) return QG_ERR_RCCL;
@@ -725,7 +804,7 @@ int SpectralSolver::solve(const double *in1, const double *in2, double *out1, do
     } else if (gather) {  // one-rank ring: still drive the transport (grec aliases rec)
         QG_CHECK(gather(user, a.rec, grec_buf_, a.rec_stride, s));
     }
-    spec_pin<<<1, PIN_THREADS, 0, s>>>(a);
+    spec_pin<<<pin_kblocks(a.KH), PIN_THREADS, 0, s>>>(a);
     QG_LAUNCH_CHECK();
     QG_CHECK(dispatch_pass(true, a, s));
     return QG_OK;

@@ -54,9 +54,10 @@ struct SpecArgs {
     const double *grec;       // gathered records [nranks] (== rec when nranks == 1)
     int64_t rec_stride;       // doubles per record
     double2 *EXT;             // [2 (Uext, Wext)][2][KS]
-    double *line;             // [P] local segment of the singular line (already / M)
-    double *scal;             // [0] = delta, [1] = pin
-    double *work;             // pin-kernel scratch: >= P_total doubles
+    double *hline;            // [P] k = 0 Poisson line h_j of this rank (pass A)
+    double *line;             // [P] centred local part of the singular line, scaled (carry)
+    double *scal;             // [0] = delta, [1] = pin, [2] [3]: singular-line offset, slope
+    double *pinpart;          // per-workgroup parts of the pin value (spec_pin -> pass B)
 };
 
 // record layout (doubles)
@@ -64,9 +65,10 @@ __host__ __device__ inline int64_t rec_AU(int KS) { return 0; }                 
 __host__ __device__ inline int64_t rec_AW(int KS) { return 4 * (int64_t)KS; }  // [2][KS] double2
 __host__ __device__ inline int64_t rec_ULS0(int KS) { return 8 * (int64_t)KS; }  // [KS] double2 (sys 0)
 __host__ __device__ inline int64_t rec_UIN0(int KS) { return 10 * (int64_t)KS; } // [KS] double2 (sys 0)
-__host__ __device__ inline int64_t rec_DSUM(int KS) { return 12 * (int64_t)KS; } // 2 doubles
-__host__ __device__ inline int64_t rec_HLINE(int KS) { return 12 * (int64_t)KS + 2; }  // [P]
-__host__ __device__ inline int64_t rec_size(int KS, int64_t P) { return 12 * (int64_t)KS + 2 + ((P + 1) & ~1LL); }
+// [0] sum of the k = 0 Poisson line (-> delta), [1] H = its local total, [2] Q = sum of its
+// local prefix sums (the singular line's cross-rank affine correction), [3] unused
+__host__ __device__ inline int64_t rec_DSUM(int KS) { return 12 * (int64_t)KS; }
+__host__ __device__ inline int64_t rec_size(int KS, int64_t P) { (void)P; return 12 * (int64_t)KS + 4; }
 
 class SpectralSolver {
 public:

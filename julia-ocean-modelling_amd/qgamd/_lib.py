@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libqgmi355.so")
+# QGMI355_LIB: alternative build of the same library (tuning experiments); never a fallback
+LIB_PATH = os.environ.get("QGMI355_LIB") or os.path.join(PKG_DIR, "lib", "libqgmi355.so")
 
 QG_OK = 0
 QG_SOLVER_SPECTRAL = 0

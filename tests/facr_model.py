@@ -37,7 +37,13 @@ def rank_pass_a(f1, f2, M, dx, alphas, pinned0, L, Pl, Pt):
     B = [(Z[:KH] + np.conj(Z[(M - kk) % M])) / 2, (Z[:KH] - np.conj(Z[(M - kk) % M])) / (2j)]
     Nc = Pl // L
     st = []
-    rec = {"dsum": float(np.sum(np.real(B[0][0]))) if pinned0 else 0.0, "hline": np.real(B[0][0]).copy()}
+    rec = {"dsum": float(np.sum(np.real(B[0][0]))) if pinned0 else 0.0}
+    # local part of the singular k = 0 Poisson line (spec_carry's extra workgroup): centred
+    # exclusive prefix sums of the local prefix sums; H, Q go into the record
+    h = np.real(B[0][0]).copy()
+    S = np.cumsum(h)
+    rec["H"], rec["Q"] = float(S[-1]), float(S.sum())
+    xc = np.concatenate([[0.0], np.cumsum(S - S.mean())[:-1]]) * dx * dx / M
     for s in range(2):
         c = coefs(M, dx, alphas[s], pinned0 and s == 0, L, Pl, Pt)
         U = np.zeros((KH, Pl), complex)
@@ -70,6 +76,7 @@ def rank_pass_a(f1, f2, M, dx, alphas, pinned0, L, Pl, Pt):
         if s == 0:
             rec["ULS0"], rec["UIN0"] = ULS[0].copy(), UIN[0].copy()
         st.append(dict(c=c, U=U, UIN=UIN, WIN=WIN))
+    st[0]["xc"] = xc
     return rec, st
 
 
@@ -128,13 +135,19 @@ def rank_pass_b(recs, rank, st, M, dx, pinned0, L, Pl, Pt, P_fwd):
                     with np.errstate(divide="ignore"):
                         cu = cu / np.where(c["r"] == 0, 1, c["r"])
                     Xs[:, j] = w
-        if dl:  # singular line over the global extent
-            h = np.concatenate([rc["hline"] for rc in recs])
-            h[0] += delta
-            S = np.cumsum(h)
-            D = S - S.mean()
-            Xl = np.concatenate([[0.0], np.cumsum(D)[:-1]]) * dx * dx / M
-            Xs[0] = Xl[rank * Pl:(rank + 1) * Pl]
+        if dl:  # singular line: local part + affine cross-rank correction (spec_pin)
+            C, tot = 0.0, 0.0
+            for rc in recs:
+                tot += Pl * C + rc["Q"]
+                C += rc["H"]
+            m = tot / Pt
+            Cr, X0 = 0.0, 0.0
+            for rc in recs[:rank]:
+                X0 += (Pl * Cr + rc["Q"]) - Pl * m
+                Cr += rc["H"]
+            mloc = recs[rank]["Q"] / Pl
+            sc = dx * dx / M
+            Xs[0] = (sc * X0 + np.arange(Pl) * (sc * ((Cr - m) + mloc))) + st[0]["xc"]
         X.append(Xs)
     Zp = np.zeros((M, Pl), complex)
     k = np.arange(KH)
