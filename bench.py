@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--chunk-rows", type=int, default=0)
     ap.add_argument("--cpu-steps", type=int, default=10, help="CPU-oracle sample steps (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all threads OpenMP offers")
+    ap.add_argument("--comm-self", action="store_true",
+                    help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
 
 
@@ -89,6 +91,11 @@ def main():
     n = args.n
     m = qgamd.bench_model(n, dt=args.dt, P=n * world)
     st = qgamd.State(m, chunk_rows=args.chunk_rows, P_local=n)
+    if world == 1 and args.comm_self:
+        import ctypes as C
+        buf = C.create_string_buffer(128)
+        qgamd._lib.call("qg_comm_unique_id", buf)
+        st.comm_init(1, 0, buf.raw)
     if world > 1:
         uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
         if rank == 0:
@@ -170,7 +177,8 @@ def main():
                         f"{args.dt:g} s, bench params of julia_bench_parts.jl:6-18",
             "grid_per_gpu": [n, n],
             "global_grid": [n, n * world],
-            "parallelism": f"y-slab x{world}" if world > 1 else "single GPU",
+            "parallelism": f"y-slab x{world}" if world > 1 else ("single GPU, 1-rank RCCL ring" if args.comm_self
+                                                                 else "single GPU"),
             "solver": "spectral (x-DFT + parallel cyclic tridiagonal in y, direct)",
             "finite": finite,
         },

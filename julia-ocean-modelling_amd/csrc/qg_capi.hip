@@ -15,6 +15,8 @@ int comm_destroy(void *comm);
 int comm_allgather(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
 int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
               hipStream_t s);
+int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t M,
+                  int64_t P, hipStream_t s, bool ghost_f2);
 int comm_init(void **comm, int nranks, int rank, const char id[128]);
 int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sendrecv_fn sr, void *user);
 int comm_unique_id(char out[128]);
@@ -41,6 +43,10 @@ struct qg_ctx {
     bool distributed = false;    // a transport is attached: halo exchange + record gather path
     void *comm = nullptr;        // RCCL communicator wrapper (multi-GPU)
     double *halo = nullptr;      // received halo rows (multi-GPU)
+    // multi-GPU: the ghost rows of the fields a step writes are refreshed lazily, grouped
+    // with the next step's halo exchange (one RCCL launch) or by qg_synchronize /
+    // qg_canonicalize
+    bool ghosts_pending = false;
     std::unique_ptr<SpectralSolver> spec;
     std::unique_ptr<PcgSolver> pcg;
     int last_status = QG_OK;  // of the last solve (PCG: QG_ERR_NOT_CONVERGED is kept here)
@@ -189,6 +195,26 @@ static void fill_wrap_rows(const qg_ctx *c, const double *base, RowSrc &rs) {
     for (int h = 0; h < 4; ++h) rs.halo[h] = base + fidx(1, rows[h] + 1, ld);
 }
 
+// ---- multi-GPU ghost rows --------------------------------------------------------------
+// the newest zeta, psi and F (both layers): the fields whose ghost rows a step leaves stale
+static int newest_fields(qg_ctx *c, double *f[6]) {
+    for (int l = 0; l < 2; ++l) {
+        f[l] = c->field(c->zeta, l, c->heads[0]);
+        f[2 + l] = c->field(c->psi, l, c->heads[1]);
+        f[4 + l] = c->field(c->fst, l, c->heads[2]);
+    }
+    return 6;
+}
+
+static int flush_ghosts(qg_ctx *c) {
+    if (!c->distributed || !c->ghosts_pending) return QG_OK;
+    double *f[6];
+    const int n = newest_fields(c, f);
+    QG_CHECK(comm_exchange(c->comm, nullptr, 0, nullptr, f, n, c->p.M, c->p.P, c->stream, false));
+    c->ghosts_pending = false;
+    return QG_OK;
+}
+
 int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     if (!c || timestep < 1) return QG_ERR_INVALID_ARG;
     if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
@@ -224,22 +250,25 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
             fill_wrap_rows(c, a.zeta[l], a.zeta_rows[l]);
             fill_wrap_rows(c, a.psi[l], a.psi_rows[l]);
         }
+        QG_CHECK(launch_tendency(a, c->stream));
     } else {
-        // halo rows of psi (depth 2) and zeta (depth 1) from the neighbouring slabs
-        double *fields[4] = {const_cast<double *>(a.psi[0]), const_cast<double *>(a.psi[1]),
-                             const_cast<double *>(a.zeta[0]), const_cast<double *>(a.zeta[1])};
-        QG_CHECK(comm_halo(c->comm, fields, 4, p.M, p.P, 2, c->halo, c->stream));
+        // halo rows of psi (depth 2; zeta uses the inner two) from the neighbouring slabs,
+        // grouped with the pending ghost-row refresh of the previous step's outputs
+        double *f2[4] = {const_cast<double *>(a.psi[0]), const_cast<double *>(a.psi[1]),
+                         const_cast<double *>(a.zeta[0]), const_cast<double *>(a.zeta[1])};
+        // (the f2 fields are the newest psi and zeta: their ghost rows come from the halo rows)
+        double *f1[2] = {c->field(c->fst, 0, fh), c->field(c->fst, 1, fh)};
+        const int n1 = c->ghosts_pending ? 2 : 0;
+        QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, p.M, p.P, c->stream, c->ghosts_pending));
+        c->ghosts_pending = false;
         const int64_t row = p.M + 2;  // halo buffer: [field][4 rows][M+2]; +1 = interior start
         for (int l = 0; l < 2; ++l)
             for (int h = 0; h < 4; ++h) {
                 a.psi_rows[l].halo[h] = c->halo + ((size_t)(l * 4 + h)) * row + 1;
                 a.zeta_rows[l].halo[h] = c->halo + ((size_t)((2 + l) * 4 + h)) * row + 1;
             }
-    }
-    QG_CHECK(launch_tendency(a, c->stream));
-    if (c->distributed) {  // ghost rows of the new zeta and F from the neighbours
-        double *fields[4] = {a.zeta_out[0], a.zeta_out[1], a.f_out[0], a.f_out[1]};
-        QG_CHECK(comm_halo(c->comm, fields, 4, p.M, p.P, -1, nullptr, c->stream));
+        QG_CHECK(launch_tendency(a, c->stream));
+        c->ghosts_pending = true;
     }
     c->heads[0] = zn;
     c->heads[2] = fn;
@@ -264,11 +293,8 @@ int qg_evolve_psi(qg_ctx *c) {
         QG_CHECK(c->spec->solve(z1, z2, o1, o2, !c->distributed, c->stream,
                                 c->distributed ? comm_allgather : nullptr, c->comm));
     }
-    if (c->distributed) {  // ghost rows of the new psi from the neighbours (drop-in ghost ring)
-        double *fields[2] = {o1, o2};
-        QG_CHECK(comm_halo(c->comm, fields, 2, c->p.M, c->p.P, -1, nullptr, c->stream));
-    }
     c->heads[1] = pn;
+    if (c->distributed) c->ghosts_pending = true;  // psi's ghost rows: with the next exchange
     return c->pcg ? c->last_status : QG_OK;
 }
 
@@ -287,6 +313,7 @@ int qg_canonicalize(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     if (!c->zeta) return QG_ERR_NOT_BOUND;
     QG_HIP(hipSetDevice(c->device));
+    QG_CHECK(flush_ghosts(c));  // pending ghost-ring refreshes
     double *bases[3] = {c->zeta, c->psi, c->fst};
     double *tmp = nullptr;
     const size_t bytes = sizeof(double) * c->F * 6;
@@ -340,6 +367,7 @@ int qg_solver_stats(qg_ctx *c, int *it_poisson, int *it_helm, double *relres_p, 
 int qg_synchronize(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     QG_HIP(hipSetDevice(c->device));
+    QG_CHECK(flush_ghosts(c));
     QG_HIP(hipStreamSynchronize(c->stream));
     return QG_OK;
 }

@@ -2,7 +2,8 @@
 //   - halo rows for the tendency stencil: ncclSend/ncclRecv of whole contiguous rows to the
 //     two ring neighbours inside one group (each row already carries its x-ghosts, so the
 //     diagonal corners the Arakawa Jacobian reads arrive with it);
-//   - ghost-row refresh of freshly written fields (drop-in ghost ring);
+//   - ghost-row refresh of the fields written by the previous step (drop-in ghost ring),
+//     grouped with the next step's halo exchange;
 //   - the spectral solver's per-step all-gather of the rank records (a few hundred KB).
 #include <rccl/rccl.h>
 
@@ -18,6 +19,8 @@ struct Comm {
     qg_sendrecv_fn sr = nullptr;
     void *user = nullptr;
     int nranks = 1, rank = 0;
+    double *stage = nullptr;  // exchange staging: [to_next | to_prev | from_prev | from_next]
+    size_t stage_n = 0;
 };
 
 #define QG_NCCL(call)                                                                          \
@@ -71,6 +74,7 @@ int comm_destroy(void *comm) {
     Comm *c = static_cast<Comm *>(comm);
     if (!c) return QG_OK;
     if (c->nccl) ncclCommDestroy(c->nccl);
+    if (c->stage) (void)hipFree(c->stage);
     delete c;
     return QG_OK;
 }
@@ -84,46 +88,103 @@ int comm_allgather(void *user, const double *send, double *recv, int64_t count, 
     return QG_OK;
 }
 
-// depth == 2: fill halo_buf[f][4][M+2] with rows -2,-1 (from rank-1) and P,P+1 (from rank+1)
-// depth == -1: refresh the ghost rows (memory rows 0 and P+1) of each field in place
-int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
-              hipStream_t s) {
+// Row copies (pack / unpack of the exchange): pair k copies one row of ld doubles.
+constexpr int XMAX = 64;
+struct RowCopies {
+    const double *src[XMAX];
+    double *dst[XMAX];
+    int n;
+    int64_t ld;
+};
+
+__global__ void copy_rows_kernel(RowCopies rc) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int k = blockIdx.y;
+    if (k < rc.n && i < rc.ld) rc.dst[k][i] = rc.src[k][i];
+}
+
+static int copy_rows(const RowCopies &rc, hipStream_t s) {
+    if (rc.n == 0) return QG_OK;
+    copy_rows_kernel<<<dim3((unsigned)((rc.ld + 255) / 256), (unsigned)rc.n), 256, 0, s>>>(rc);
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+// One exchange with the two ring neighbours, as ONE message per direction: the rows are
+// packed into a staging buffer per neighbour, sent / received in one group, and unpacked.
+//   f2[0..n2): depth-2 halo -> halo_buf[f][4][M+2] = rows -2,-1 (from rank-1), P,P+1 (from
+//              rank+1); with ghost_f2 the ghost rows of f2 (rows -1 and P) are filled too
+//   f1[0..n1): refresh of the ghost rows (memory rows 0 and P+1) in place
+// Messages: [send -> next, send -> prev], [recv <- prev, recv <- next]; with two ranks
+// (prev == next) the two messages per peer match in this posting order.
+int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t M,
+                  int64_t P, hipStream_t s, bool ghost_f2) {
     Comm *c = static_cast<Comm *>(comm);
     if (!c || (!c->nccl && !c->sr)) return QG_ERR_RCCL;
+    const int rows = 2 * n2 + n1;  // rows per direction
+    if (n2 < 0 || n1 < 0 || 4 * n2 + (ghost_f2 ? 2 * n2 : 0) + 2 * n1 > XMAX) return QG_ERR_INVALID_ARG;
+    if (rows == 0) return QG_OK;
     const int G = c->nranks;
     const int next = (c->rank + 1) % G, prev = (c->rank - 1 + G) % G;
-    const size_t ld = (size_t)(M + 2);
-    // one grouped exchange; per field: [send last rows -> next, send first rows -> prev] and
-    // [recv low rows <- prev, recv high rows <- next] (this order also matches the two
-    // messages per peer correctly when prev == next, i.e. two ranks)
-    const int nmax = 4 * 16;
-    if (nfields > 16) return QG_ERR_INVALID_ARG;
-    const double *sp[nmax];
-    double *rp[nmax];
-    int64_t sc[nmax], rc[nmax];
-    int speer[nmax], rpeer[nmax];
-    int ns = 0, nr = 0;
-    for (int f = 0; f < nfields; ++f) {
-        double *b = fields[f];
-        if (depth == 2) {
-            double *lo = halo_buf + (size_t)f * 4 * ld, *hi = lo + 2 * ld;
-            sp[ns] = b + fidx(0, P - 1, ld); sc[ns] = 2 * ld; speer[ns++] = next;
-            sp[ns] = b + fidx(0, 1, ld);     sc[ns] = 2 * ld; speer[ns++] = prev;
-            rp[nr] = lo; rc[nr] = 2 * ld; rpeer[nr++] = prev;
-            rp[nr] = hi; rc[nr] = 2 * ld; rpeer[nr++] = next;
-        } else {
-            sp[ns] = b + fidx(0, P, ld); sc[ns] = ld; speer[ns++] = next;
-            sp[ns] = b + fidx(0, 1, ld); sc[ns] = ld; speer[ns++] = prev;
-            rp[nr] = b + fidx(0, 0, ld);     rc[nr] = ld; rpeer[nr++] = prev;
-            rp[nr] = b + fidx(0, P + 1, ld); rc[nr] = ld; rpeer[nr++] = next;
+    const int64_t ld = M + 2;
+    const size_t need = (size_t)4 * rows * ld;
+    if (need > c->stage_n) {
+        if (c->stage) (void)hipFree(c->stage);
+        c->stage = nullptr;
+        c->stage_n = 0;
+        QG_HIP(hipMalloc((void **)&c->stage, sizeof(double) * need));
+        c->stage_n = need;
+    }
+    double *to_next = c->stage, *to_prev = to_next + rows * ld;
+    double *from_prev = to_prev + rows * ld, *from_next = from_prev + rows * ld;
+    RowCopies pk{}, up{};
+    pk.ld = up.ld = ld;
+    int r = 0;
+    for (int f = 0; f < n2; ++f, r += 2) {
+        double *b = f2[f];
+        double *lo = halo_buf + (size_t)f * 4 * ld, *hi = lo + 2 * ld;
+        for (int q = 0; q < 2; ++q) {
+            pk.src[pk.n] = b + fidx(0, P - 1 + q, ld); pk.dst[pk.n++] = to_next + (r + q) * ld;  // rows P-2, P-1
+            pk.src[pk.n] = b + fidx(0, 1 + q, ld);     pk.dst[pk.n++] = to_prev + (r + q) * ld;  // rows 0, 1
+            up.src[up.n] = from_prev + (r + q) * ld;   up.dst[up.n++] = lo + q * ld;            // rows -2, -1
+            up.src[up.n] = from_next + (r + q) * ld;   up.dst[up.n++] = hi + q * ld;            // rows P, P+1
+        }
+        if (ghost_f2) {
+            up.src[up.n] = from_prev + (r + 1) * ld; up.dst[up.n++] = b + fidx(0, 0, ld);
+            up.src[up.n] = from_next + r * ld;       up.dst[up.n++] = b + fidx(0, P + 1, ld);
         }
     }
-    if (c->sr) return c->sr(c->user, ns, sp, sc, speer, nr, rp, rc, rpeer, s) == 0 ? QG_OK : QG_ERR_RCCL;
-    QG_NCCL(ncclGroupStart());
-    for (int k = 0; k < ns; ++k) QG_NCCL(ncclSend(sp[k], (size_t)sc[k], ncclDouble, speer[k], c->nccl, s));
-    for (int k = 0; k < nr; ++k) QG_NCCL(ncclRecv(rp[k], (size_t)rc[k], ncclDouble, rpeer[k], c->nccl, s));
-    QG_NCCL(ncclGroupEnd());
-    return QG_OK;
+    for (int f = 0; f < n1; ++f, ++r) {
+        double *b = f1[f];
+        pk.src[pk.n] = b + fidx(0, P, ld);     pk.dst[pk.n++] = to_next + r * ld;
+        pk.src[pk.n] = b + fidx(0, 1, ld);     pk.dst[pk.n++] = to_prev + r * ld;
+        up.src[up.n] = from_prev + r * ld;     up.dst[up.n++] = b + fidx(0, 0, ld);
+        up.src[up.n] = from_next + r * ld;     up.dst[up.n++] = b + fidx(0, P + 1, ld);
+    }
+    QG_CHECK(copy_rows(pk, s));
+    const int64_t cnt = (int64_t)rows * ld;
+    if (c->sr) {
+        const double *sp[2] = {to_next, to_prev};
+        double *rp[2] = {from_prev, from_next};
+        const int64_t sc[2] = {cnt, cnt}, rcnt[2] = {cnt, cnt};
+        const int speer[2] = {next, prev}, rpeer[2] = {prev, next};
+        if (c->sr(c->user, 2, sp, sc, speer, 2, rp, rcnt, rpeer, s) != 0) return QG_ERR_RCCL;
+    } else {
+        QG_NCCL(ncclGroupStart());
+        QG_NCCL(ncclSend(to_next, (size_t)cnt, ncclDouble, next, c->nccl, s));
+        QG_NCCL(ncclSend(to_prev, (size_t)cnt, ncclDouble, prev, c->nccl, s));
+        QG_NCCL(ncclRecv(from_prev, (size_t)cnt, ncclDouble, prev, c->nccl, s));
+        QG_NCCL(ncclRecv(from_next, (size_t)cnt, ncclDouble, next, c->nccl, s));
+        QG_NCCL(ncclGroupEnd());
+    }
+    return copy_rows(up, s);
+}
+
+// depth == 2: halo rows into halo_buf; depth == -1: ghost-row refresh in place
+int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
+              hipStream_t s) {
+    if (depth == 2) return comm_exchange(comm, fields, nfields, halo_buf, nullptr, 0, M, P, s, false);
+    return comm_exchange(comm, nullptr, 0, nullptr, fields, nfields, M, P, s, false);
 }
 
 }  // namespace qg

@@ -129,6 +129,7 @@ struct TendArgs {
     double beta[2];
     int ab3;                   // 0 = Euler, 1 = AB3
     int j0, j1;                // output row range [j0, j1)
+    int j2, j3;                // optional second range [j2, j3) (empty: j3 <= j2)
     int write_ghost_rows;      // single-GPU: refresh ghost rows -1 and P
     // per layer pointers (field base = element (0,0) incl. ghosts)
     const double *zeta[2];

@@ -102,8 +102,10 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
     const int64_t ld = a.ld;
     const int x0 = blockIdx.x * TX;
     const int i = x0 + t;
-    const int jb0 = a.j0 + blockIdx.y * rows_per_block;
-    const int jb1 = min(jb0 + rows_per_block, a.j1);
+    const int nA = (a.j1 - a.j0 + rows_per_block - 1) / rows_per_block;  // blocks of range 1
+    const bool second = (int)blockIdx.y >= nA;
+    const int jb0 = second ? a.j2 + ((int)blockIdx.y - nA) * rows_per_block : a.j0 + blockIdx.y * rows_per_block;
+    const int jb1 = min(jb0 + rows_per_block, second ? a.j3 : a.j1);
     if (jb0 >= jb1) return;  // uniform over the block
 
     __shared__ double sp[RP][TX + 4];
@@ -333,8 +335,8 @@ int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s) {
 
 template <int TX, int PF>
 static int launch_tend_variant(const TendArgs &a, int rows, hipStream_t s) {
-    const int nrows = a.j1 - a.j0;
-    dim3 grid((unsigned)((a.M + TX - 1) / TX), (unsigned)((nrows + rows - 1) / rows), 2);
+    const int nA = (a.j1 - a.j0 + rows - 1) / rows, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + rows - 1) / rows : 0;
+    dim3 grid((unsigned)((a.M + TX - 1) / TX), (unsigned)(nA + nB), 2);
     tendency_kernel<TX, PF><<<grid, TX, 0, s>>>(a, rows);
     QG_LAUNCH_CHECK();
     return QG_OK;
@@ -351,7 +353,7 @@ static int tend_variant() {
 }
 
 int launch_tendency(const TendArgs &a, hipStream_t s) {
-    if (a.j1 - a.j0 <= 0) return QG_OK;
+    if (a.j1 - a.j0 <= 0 && a.j3 - a.j2 <= 0) return QG_OK;
     switch (tend_variant()) {
         case 1: return launch_tend_variant<256, 1>(a, 32, s);
         case 2: return launch_tend_variant<128, 1>(a, 64, s);

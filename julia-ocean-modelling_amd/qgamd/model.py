@@ -250,14 +250,17 @@ class State:
         return t[torch.tensor(order, device=t.device)]
 
     def current(self, which, layer):
-        """Reference ``X[:, :, layer, 1]`` (layer 1-based) as a (P+2, M+2) view."""
+        """Reference ``X[:, :, layer, 1]`` (layer 1-based) as a (P+2, M+2) view (multi-GPU:
+        ghost rows current after synchronize())."""
         return getattr(self, which)[self.slot(which, 1), layer - 1]
 
     def canonicalize(self):
         call("qg_canonicalize", self._ctx)
 
     def to_numpy(self, which):
-        """Reference-ordered numpy array of shape (M+2, P+2, 2, 3) (Julia index order)."""
+        """Reference-ordered numpy array of shape (M+2, P+2, 2, 3) (Julia index order).
+        Synchronises first (multi-GPU: completes the lazily refreshed ghost rows)."""
+        self.synchronize()
         return self.logical(which).permute(3, 2, 1, 0).contiguous().cpu().numpy()
 
 
