@@ -14,9 +14,13 @@ __host__ __device__ inline int pin_kblocks(int KH) { return (2 * KH + PIN_THREAD
 
 template <int N>
 struct Geo {
-    static constexpr int T = N / 4 < 64 ? 64 : (N / 4 > 1024 ? 1024 : N / 4);  // threads per row
-    // one workgroup of T threads per CU (72 KB of LDS at N = 4096): registers capped at
-    // 512 / (T / 256) per lane so the whole workgroup stays resident
+    // threads per row: N/8 (one radix-8 butterfly per thread and pass: 4 passes at N = 4096).
+    // One workgroup per CU (two row buffers + twiddles = 154 KB of LDS at N = 4096);
+    // registers capped at 512 / (T / 256) per lane so the whole workgroup stays resident.
+#ifndef QG_SPEC_TDIV
+#define QG_SPEC_TDIV 8
+#endif
+    static constexpr int T = N / QG_SPEC_TDIV < 64 ? 64 : (N / QG_SPEC_TDIV > 1024 ? 1024 : N / QG_SPEC_TDIV);
     static constexpr int MINW = T / 256 < 1 ? 1 : T / 256;
     static constexpr int KH = N / 2 + 1;
     // wavenumber slots per thread over k in [0, N/2); the real Nyquist line k = N/2 rides in
