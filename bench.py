@@ -46,27 +46,53 @@ def parse():
     ap.add_argument("--chunk-rows", type=int, default=0)
     ap.add_argument("--cpu-steps", type=int, default=10, help="CPU-oracle sample steps (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all threads OpenMP offers")
+    ap.add_argument("--cpu-steps-1t", type=int, default=2, help="single-thread CPU-oracle sample steps")
+    ap.add_argument("--solver", choices=("spectral", "pcg"), default="spectral",
+                    help="streamfunction inversion: direct spectral (default) or matrix-free PCG "
+                         "preconditioned by the spectral solve")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
 
 
-def cpu_baseline(n, dt, steps, threads):
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(n, dt, steps, threads, steps_1t):
     """Time the C oracle (oracle/qg_oracle.c, OpenMP) on a bounded sample of the same
-    workload: `steps` AB3 timesteps of the same n x n F64 model after its 2 Euler steps."""
+    workload: `steps` AB3 timesteps of the same n x n F64 model after its 2 Euler steps, with
+    all threads OpenMP offers, then `steps_1t` of them on one thread (the reference's
+    1-core job, scripts/benchmarking_job.sh:13)."""
     from oracle import qg_oracle, qg_ref
 
     qg_oracle.build()
     m = qg_ref.bench_model(n, dt=dt)
-    st = qg_oracle.State(m, nthreads=threads)
-    st.run(2)  # the Euler steps (untimed)
-    t0 = time.perf_counter()
-    st.run(steps)
-    el = time.perf_counter() - t0
+
+    def timed(nthreads, k):
+        st = qg_oracle.State(m, nthreads=nthreads)
+        st.run(2)  # the Euler steps (untimed)
+        t0 = time.perf_counter()
+        st.run(k)
+        return time.perf_counter() - t0
+
+    el = timed(threads, steps)
     used = threads if threads > 0 else qg_oracle.lib().qgo_max_threads()
-    return {"value": steps / el, "unit": "timesteps/s", "cores": int(used), "kind": "port",
-            "sample": f"{steps} AB3 timesteps of the {n}x{n} F64 model (after its 2 Euler steps), "
-                      f"C oracle (exact DFT solve), {el:.2f} s wall"}
+    out = {"value": steps / el, "unit": "timesteps/s", "cores": int(used), "kind": "port",
+           "sample": f"{steps} AB3 timesteps of the {n}x{n} F64 model (after its 2 Euler steps), "
+                     f"C oracle (exact DFT solve), {el:.2f} s wall",
+           "cpu": _cpu_model(), "nproc": os.cpu_count()}
+    if steps_1t > 0:
+        el1 = timed(1, steps_1t)
+        out["single_thread"] = {"value": steps_1t / el1, "unit": "timesteps/s", "cores": 1,
+                                "sample": f"{steps_1t} AB3 timestep(s), same model, 1 thread, {el1:.2f} s wall"}
+    return out
 
 
 def main():
@@ -90,7 +116,10 @@ def main():
 
     n = args.n
     m = qgamd.bench_model(n, dt=args.dt, P=n * world)
-    st = qgamd.State(m, chunk_rows=args.chunk_rows, P_local=n)
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter()
+    solver = qgamd._lib.QG_SOLVER_PCG if args.solver == "pcg" else qgamd._lib.QG_SOLVER_SPECTRAL
+    st = qgamd.State(m, solver=solver, chunk_rows=args.chunk_rows, P_local=n)
     if world == 1 and args.comm_self:
         import ctypes as C
         buf = C.create_string_buffer(128)
@@ -106,6 +135,8 @@ def main():
         dist.broadcast(uid, 0)
         st.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
     st.initialise()
+    torch.cuda.synchronize()
+    setup_ms = (time.perf_counter() - t_setup) * 1e3
 
     t = 1
     for _ in range(args.warmup):
@@ -136,6 +167,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
+    step_ev_ms = sorted(e[0].elapsed_time(e[2]) for e in ev)
+    median_ms = step_ev_ms[K // 2]
     tend_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / K
     solve_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / K
     finite = bool(torch.isfinite(st.current("psi", 1)).all().item())
@@ -166,6 +199,8 @@ def main():
         "steps": K,
         "warmup": args.warmup,
         "ms_per_step": ms,
+        "ms_per_step_median": median_ms,
+        "setup_ms": setup_ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -179,7 +214,8 @@ def main():
             "global_grid": [n, n * world],
             "parallelism": f"y-slab x{world}" if world > 1 else ("single GPU, 1-rank RCCL ring" if args.comm_self
                                                                  else "single GPU"),
-            "solver": "spectral (x-DFT + parallel cyclic tridiagonal in y, direct)",
+            "solver": ("spectral (x-DFT + parallel cyclic tridiagonal in y, direct)" if args.solver == "spectral"
+                       else "matrix-free PCG on the 5-point operator, spectral preconditioner"),
             "finite": finite,
         },
         "roofline": {
@@ -199,7 +235,7 @@ def main():
         },
     }
     if args.cpu_steps > 0 and world == 1:
-        out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads)
+        out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads, args.cpu_steps_1t)
     else:
         out["cpu_baseline"] = None
     print(json.dumps(out), flush=True)

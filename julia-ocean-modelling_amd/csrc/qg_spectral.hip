@@ -462,6 +462,7 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
 // carry-in state of line (s, k) entering chunk c: cu = r^L u_in, w = w_in (see header)
 __device__ __forceinline__ void chunk_carry(const SpecArgs &a, int s, int k, int c, double delta, bool inject,
                                             double2 &cu, double2 &w) {
+
     const Coef cf = a.coef[s * a.KS + k];
     const double2 Ue = a.EXT[(size_t)s * a.KS + k], We = a.EXT[(size_t)(2 + s) * a.KS + k];
     const int64_t n = (int64_t)c * a.L;
@@ -501,6 +502,22 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     const bool sing = a.pinned0;  // (s = 0, k = 0) is the singular line, served by a.line
     const double line0 = a.scal[2], line1 = a.scal[3];
 
+    // register prefetch of the next row of u (in flight across this row's FFT).  Slot (0, t=0)
+    // packs the real lines k = 0 (.x) and k = N/2 (.y).
+    double2 upf[KQ][2];
+    auto load_u = [&](int j) {
+        const double2 *Urow = a.U + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+            const int k = t + q * T;
+            if (NH % T == 0 || k < NH) {
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    upf[q][s] = k == 0 ? make_double2(Urow[s * KS].x, Urow[s * KS + NH].x) : Urow[s * KS + k];
+            }
+        }
+    };
+    load_u(s0);  // first row in flight while the chunk carries are computed
     // per line: carried term cu = r^(e+1-j) u_in and forward-filter state w.  Slot (0, t = 0)
     // packs the real lines k = 0 (.x) and k = N/2 (.y).
     double2 cu[KQ][2], w[KQ][2];
@@ -524,36 +541,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             }
         }
     }
-    // register prefetch of the next row of u (in flight across this row's FFT).  Slot (0, t=0)
-    // packs the real lines k = 0 (.x) and k = N/2 (.y).
-    double2 upf[KQ][2];
-    auto load_u = [&](int j) {
-        const double2 *Urow = a.U + (size_t)j * 2 * KS;
-#pragma unroll
-        for (int q = 0; q < KQ; ++q) {
-            const int k = t + q * T;
-            if (NH % T == 0 || k < NH) {
-#pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    upf[q][s] = k == 0 ? make_double2(Urow[s * KS].x, Urow[s * KS + NH].x) : Urow[s * KS + k];
-            }
-        }
-    };
-#ifndef QG_PASSB_NO_PREFETCH
-    load_u(s0);
-#endif
     for (int j = s0; j <= e; ++j) {
-#ifdef QG_PASSB_NO_PREFETCH
-        load_u(j);
-#endif
         double2 ucur[KQ][2];
 #pragma unroll
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
             for (int s = 0; s < 2; ++s) ucur[q][s] = upf[q][s];
-#ifndef QG_PASSB_NO_PREFETCH
         if (j < e) load_u(j + 1);
-#endif
         // compiler memory barrier: re-read the (L1-resident) coefficients every row instead of
         // hoisting them into registers, which would spill at this occupancy
         asm volatile("" ::: "memory");
