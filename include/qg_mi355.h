@@ -127,6 +127,17 @@ int qg_get_stats(qg_ctx *ctx, qg_stats *out);
 int qg_solver_stats(qg_ctx *ctx, int *it_poisson, int *it_helm, double *relres_p, double *relres_h);
 int qg_synchronize(qg_ctx *ctx);
 
+/* ---- snapshot output (run_model.jl:55-95 writes zeta[:,:,:,1], psi[:,:,:,1] every
+ * sample_timestep steps) -----------------------------------------------------------------
+ * qg_snapshot enqueues, in stream order, a device copy of the newest zeta and psi (both
+ * layers, ghost ring included: 2 x (M+2) x (P+2) doubles each, the reference's
+ * zeta[:,:,:,1] layout) into a library-owned staging buffer, then returns; a copy stream
+ * moves the staging buffer to the caller's HOST buffers (page-locked memory gives an
+ * asynchronous copy) while the caller keeps stepping.  A second qg_snapshot first waits for
+ * the previous copy.  qg_snapshot_wait blocks until the host buffers are complete.          */
+int qg_snapshot(qg_ctx *ctx, double *host_zeta, double *host_psi);
+int qg_snapshot_wait(qg_ctx *ctx);
+
 /* ---- multi-GPU (one rank per GPU, slab decomposition in y) ---------------------------
  * Rank r owns global rows [r*P, (r+1)*P) of a global M x (nranks*P) grid; the y direction is
  * periodic over the ring of ranks.  Per step the library exchanges halo rows with the two

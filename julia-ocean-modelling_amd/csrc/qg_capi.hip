@@ -47,6 +47,11 @@ struct qg_ctx {
     // with the next step's halo exchange (one RCCL launch) or by qg_synchronize /
     // qg_canonicalize
     bool ghosts_pending = false;
+    // snapshots: device staging buffer [zeta 2 layers | psi 2 layers], copy stream + events
+    double *snap = nullptr;
+    hipStream_t snap_stream = nullptr;
+    hipEvent_t snap_ready = nullptr, snap_done = nullptr;
+    bool snap_inflight = false;
     std::unique_ptr<SpectralSolver> spec;
     std::unique_ptr<PcgSolver> pcg;
     int last_status = QG_OK;  // of the last solve (PCG: QG_ERR_NOT_CONVERGED is kept here)
@@ -144,6 +149,11 @@ int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out) {
 int qg_destroy(qg_ctx *c) {
     if (!c) return QG_OK;
     (void)hipSetDevice(c->device);
+    if (c->snap_stream) (void)hipStreamSynchronize(c->snap_stream);
+    if (c->snap) (void)hipFree(c->snap);
+    if (c->snap_ready) (void)hipEventDestroy(c->snap_ready);
+    if (c->snap_done) (void)hipEventDestroy(c->snap_done);
+    if (c->snap_stream) (void)hipStreamDestroy(c->snap_stream);
     if (c->comm) comm_destroy(c->comm);
     if (c->halo) (void)hipFree(c->halo);
     delete c;
@@ -361,6 +371,43 @@ int qg_solver_stats(qg_ctx *c, int *it_poisson, int *it_helm, double *relres_p, 
     if (it_helm) *it_helm = st.iters[1];
     if (relres_p) *relres_p = st.relres[0];
     if (relres_h) *relres_h = st.relres[1];
+    return QG_OK;
+}
+
+int qg_snapshot(qg_ctx *c, double *host_zeta, double *host_psi) {
+    if (!c || !host_zeta || !host_psi) return QG_ERR_INVALID_ARG;
+    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
+    QG_HIP(hipSetDevice(c->device));
+    if (!c->snap) {
+        QG_HIP(hipMalloc((void **)&c->snap, sizeof(double) * 4 * c->F));
+        QG_HIP(hipStreamCreateWithFlags(&c->snap_stream, hipStreamNonBlocking));
+        QG_HIP(hipEventCreateWithFlags(&c->snap_ready, hipEventDisableTiming));
+        QG_HIP(hipEventCreateWithFlags(&c->snap_done, hipEventDisableTiming));
+    }
+    QG_CHECK(flush_ghosts(c));  // multi-GPU: the ghost rows of the newest fields
+    if (c->snap_inflight) QG_HIP(hipStreamWaitEvent(c->stream, c->snap_done, 0));  // staging free
+    const size_t fb = sizeof(double) * c->F;
+    for (int l = 0; l < 2; ++l) {
+        QG_HIP(hipMemcpyAsync(c->snap + l * c->F, c->field(c->zeta, l, c->heads[0]), fb, hipMemcpyDeviceToDevice,
+                              c->stream));
+        QG_HIP(hipMemcpyAsync(c->snap + (2 + l) * c->F, c->field(c->psi, l, c->heads[1]), fb,
+                              hipMemcpyDeviceToDevice, c->stream));
+    }
+    QG_HIP(hipEventRecord(c->snap_ready, c->stream));
+    QG_HIP(hipStreamWaitEvent(c->snap_stream, c->snap_ready, 0));
+    QG_HIP(hipMemcpyAsync(host_zeta, c->snap, 2 * fb, hipMemcpyDeviceToHost, c->snap_stream));
+    QG_HIP(hipMemcpyAsync(host_psi, c->snap + 2 * c->F, 2 * fb, hipMemcpyDeviceToHost, c->snap_stream));
+    QG_HIP(hipEventRecord(c->snap_done, c->snap_stream));
+    c->snap_inflight = true;
+    return QG_OK;
+}
+
+int qg_snapshot_wait(qg_ctx *c) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    if (!c->snap_inflight) return QG_OK;
+    QG_HIP(hipSetDevice(c->device));
+    QG_HIP(hipEventSynchronize(c->snap_done));
+    c->snap_inflight = false;
     return QG_OK;
 }
 

@@ -141,6 +141,45 @@ function stats(s::QGState)
     r[]
 end
 
+# --- snapshot output: run_model (run_model.jl:55-95) ---------------------------------------
+"""`snapshot!(s, zeta_host, psi_host)`: enqueue a copy of the newest `zeta[:,:,:,1]`,
+`psi[:,:,:,1]` into (M+2, P+2, 2) host arrays (page-locked via `AMDGPU.Mem.pin` for an
+asynchronous copy); `snapshot_wait(s)` blocks until they are complete."""
+snapshot!(s::QGState, zh::Array{Float64,3}, ph::Array{Float64,3}) =
+    @qgcheck qg_snapshot ccall((:qg_snapshot, libqg), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}),
+                               s.ctx, zh, ph)
+snapshot_wait(s::QGState) = @qgcheck qg_snapshot_wait ccall((:qg_snapshot_wait, libqg), Cint, (Ptr{Cvoid},), s.ctx)
+
+"""`run_model(model, file_name, save_results; write)` -- the reference driver with snapshots.
+`write(file_name, key, value)` stores one entry (default: the reference's JLD, if loaded)."""
+function run_model(model, file_name::String, save_results::Bool;
+                   write=(f, k, v) -> Main.JLD.jldopen(io -> Main.JLD.write(io, k, v), f, isfile(f) ? "r+" : "w"),
+                   kw...)
+    total_steps = floor(Int, model.T / model.dt)
+    sample_timestep = 2 * floor(Int, 86400.0 / model.dt)           # run_model.jl:59
+    s = initialise_model(model; kw...)
+    shape = (model.M + 2, model.P + 2, 2)
+    zh, ph = Array{Float64}(undef, shape), Array{Float64}(undef, shape)
+    if save_results
+        snapshot!(s, zh, ph); snapshot_wait(s)
+        write(file_name, "zeta_0", copy(zh)); write(file_name, "psi_0", copy(ph))
+        write(file_name, "metadata", Dict("dt" => model.dt, "T" => model.T, "sample_interval" => 86400.0,
+                                          "sample_timestep" => floor(Int, 86400.0 / model.dt),
+                                          "total_steps" => total_steps))
+    end
+    for t in 1:total_steps
+        evolve_zeta!(model, s, t)
+        evolve_psi!(model, s)
+        if save_results && t % sample_timestep == 0
+            snapshot!(s, zh, ph); snapshot_wait(s)
+            write(file_name, "zeta_$t", copy(zh)); write(file_name, "psi_$t", copy(ph))
+        end
+    end
+    canonical!(s)
+    AMDGPU.synchronize()
+    (s.zeta, s.psi)
+end
+
 # --- solver handles: the get_*_cholesky analogues ----------------------------------------
 mutable struct QGSolverPair
     h::Ptr{Cvoid}

@@ -11,9 +11,11 @@ from .model import (BaroclinicModel, PairSolver, State, bench_model, cd, device_
                     evolve_psi_, evolve_zeta_, get_helmholtz_cholesky, get_poisson_cholesky,
                     initialise_model, J, laplace_5p, make_model, run_model_no_output,
                     sp_solve_modified_helmholtz, sp_solve_poisson, update_doubly_periodic_bc_)
+from .run import SnapshotWriter, create_metadata, log_model_params, run_model
 
 __all__ = ["BaroclinicModel", "PairSolver", "State", "bench_model", "cd", "device_zeros",
            "evolve_psi_", "evolve_zeta_", "get_helmholtz_cholesky", "get_poisson_cholesky",
            "initialise_model", "J", "laplace_5p", "make_model", "run_model_no_output",
            "sp_solve_modified_helmholtz", "sp_solve_poisson", "update_doubly_periodic_bc_",
+           "run_model", "create_metadata", "log_model_params", "SnapshotWriter",
            "LIB_PATH", "QGError", "lib"]

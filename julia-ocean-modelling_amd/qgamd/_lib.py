@@ -67,6 +67,8 @@ SIGNATURES = [
     ("qg_solver_stats", C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
                                   C.POINTER(C.c_double)]),
     ("qg_synchronize", C.c_int, [_vp]),
+    ("qg_snapshot", C.c_int, [_vp, _vp, _vp]),
+    ("qg_snapshot_wait", C.c_int, [_vp]),
     ("qg_comm_unique_id", C.c_int, [C.c_char_p]),
     ("qg_comm_init", C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
     ("qg_comm_init_host", C.c_int, [_vp, C.c_int, C.c_int, AllgatherFn, SendrecvFn, _vp]),

@@ -76,3 +76,24 @@ def test_create_rejects_bad_params_without_gpu(qglib):
     ctx = C.c_void_p()
     # M = 0 is rejected before any device work
     assert qglib.qg_create(C.byref(p), 0, None, C.byref(ctx)) == -1
+
+
+def test_run_model_metadata_and_log_cpu():
+    """create_metadata / log_model_params (run_model.jl:6-39) on the reference's own main()
+    parameters (run_model.jl:98-112): no GPU needed."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "julia-ocean-modelling_amd"))
+    import qgamd
+    KM, MIN, YEAR = 1000.0, 60.0, 365 * 86400.0
+    M = 512
+    dx = 4000 * KM / M
+    P = int(2000 * KM / dx)
+    m = qgamd.make_model(1 * KM, 2 * KM, 2e-11, 4000 * KM, 2000 * KM, 5 * MIN, 8 * YEAR, 0.1, M, P, dx, 100.0,
+                         1e-8, 40 * KM, 1e-2)
+    md = qgamd.create_metadata(m)
+    assert md == {"dt": 300.0, "T": 8 * YEAR, "sample_interval": 86400.0, "sample_timestep": 288,
+                  "total_steps": 840960}
+    lines = []
+    qgamd.log_model_params(m, lines.append)
+    assert lines[0] == "Parameters:" and lines[-1] == "Total steps = 840960\n"
+    assert lines[8:10] == ["M = 512", "P = 256"]
