@@ -8,7 +8,13 @@
 
 namespace qg {
 
-constexpr int CARRY_WAVES = 8;
+#ifndef QG_CARRY_WAVES
+#define QG_CARRY_WAVES 8
+#endif
+#ifndef QG_CARRY_KB
+#define QG_CARRY_KB 16
+#endif
+constexpr int CARRY_WAVES = QG_CARRY_WAVES;
 constexpr int PIN_THREADS = 256;
 __host__ __device__ inline int pin_kblocks(int KH) { return (2 * KH + PIN_THREADS - 1) / PIN_THREADS; }
 
@@ -268,17 +274,26 @@ __device__ void local_line(const SpecArgs &a, double *red, double *tile) {
 //   v_c = ULS_c + q v_{c+1}, v_Nc = 0      UIN_c = v_{c+1},  AU = v_0
 //   w_c = (WLS_c + gam UIN_c) + q w_{c-1}   WIN_c = w_{c-1},  AW = w_{Nc-1}
 // ------------------------------------------------------------------------------------
-constexpr int CARRY_KB = 16;
+constexpr int CARRY_KB = QG_CARRY_KB;
 constexpr int CARRY_SEG = CARRY_WAVES * (64 / CARRY_KB);
+constexpr int CARRY_REG = 8;  // chunks per segment held in registers
 
 __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
     __shared__ double2 agg[CARRY_SEG][CARRY_KB];
     __shared__ double qlen_s[CARRY_SEG][CARRY_KB];
+    constexpr int NT = 64 * CARRY_WAVES;
     if ((int)blockIdx.x == (a.KH + CARRY_KB - 1) / CARRY_KB) {  // the extra column
-        if (blockIdx.y == 0 && a.pinned0) {
-            __shared__ double red[CARRY_WAVES];
-            __shared__ double tile[64 * CARRY_WAVES * LINE_PER * 17 / 16];
-            local_line<64 * CARRY_WAVES>(a, red, tile);
+        __shared__ double red[CARRY_WAVES];
+        if (blockIdx.y == 0) {
+            if (a.pinned0) {
+                __shared__ double tile[NT * LINE_PER * 17 / 16];
+                local_line<NT>(a, red, tile);
+            }
+        } else {  // sum of the k = 0 Poisson line over this rank (-> delta), fixed order
+            double d = 0;
+            for (int c = threadIdx.x; c < a.Nc; c += NT) d += a.dcpart[c];
+            d = block_sum<NT>(d, red);
+            if (threadIdx.x == 0) a.rec[rec_DSUM(a.KS)] = d;
         }
         return;
     }
@@ -296,14 +311,34 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
     }
     auto at = [&](const double2 *base, int c) { return base[((size_t)c * 2 + s) * KS + k]; };
     auto put = [&](double2 *base, int c, double2 v) { base[((size_t)c * 2 + s) * KS + k] = v; };
+    // the segment's summaries, loaded once (all loads in flight together) when they fit in
+    // registers; longer segments stream them from memory
+    const bool inreg = SL <= CARRY_REG;
+    double2 uls[CARRY_REG], wls[CARRY_REG], uin[CARRY_REG];
+    if (ok && inreg) {
+#pragma unroll
+        for (int m = 0; m < CARRY_REG; ++m) {
+            const int c = c0 + m;
+            uls[m] = c < c1 ? at(a.ULS, c) : make_double2(0, 0);
+            wls[m] = c < c1 ? at(a.WLS, c) : make_double2(0, 0);
+        }
+    }
 
     double2 v = make_double2(0, 0);
     double qlen = 1;
     if (ok) {
-#pragma unroll 4
-        for (int c = c1 - 1; c >= c0; --c) {
-            v = cfma(q, v, at(a.ULS, c));
-            qlen *= q;
+        if (inreg) {
+#pragma unroll
+            for (int m = CARRY_REG - 1; m >= 0; --m)
+                if (c0 + m < c1) {
+                    v = cfma(q, v, uls[m]);
+                    qlen *= q;
+                }
+        } else {
+            for (int c = c1 - 1; c >= c0; --c) {
+                v = cfma(q, v, at(a.ULS, c));
+                qlen *= q;
+            }
         }
     }
     agg[seg][kk] = v;
@@ -316,21 +351,30 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
     double2 bsum = make_double2(0, 0);
     double wq = 1;
     v = vin;
+    auto back = [&](int c, double2 wl, double2 ul) {  // UIN_c, the W aggregate term, v_c
+        put(a.UIN, c, v);
+        const double2 wt = cfma(gam, v, wl);
+        bsum = cfma(wq, wt, bsum);
+        wq *= q;
+        v = cfma(q, v, ul);
+    };
     if (ok) {
-#pragma unroll 4
-        for (int c = c1 - 1; c >= c0; --c) {
-            put(a.UIN, c, v);
-            const double2 wt = cfma(gam, v, at(a.WLS, c));
-            bsum = cfma(wq, wt, bsum);
-            wq *= q;
-            v = cfma(q, v, at(a.ULS, c));
+        if (inreg) {
+#pragma unroll
+            for (int m = CARRY_REG - 1; m >= 0; --m)
+                if (c0 + m < c1) {
+                    uin[m] = v;
+                    back(c0 + m, wls[m], uls[m]);
+                }
+        } else {
+            for (int c = c1 - 1; c >= c0; --c) back(c, at(a.WLS, c), at(a.ULS, c));
         }
     }
     if (seg == 0 && ok) {
         reinterpret_cast<double2 *>(a.rec + rec_AU(KS))[s * KS + k] = v;
         if (s == 0) {
-            reinterpret_cast<double2 *>(a.rec + rec_ULS0(KS))[k] = at(a.ULS, 0);
-            reinterpret_cast<double2 *>(a.rec + rec_UIN0(KS))[k] = at(a.UIN, 0);
+            reinterpret_cast<double2 *>(a.rec + rec_ULS0(KS))[k] = inreg ? uls[0] : at(a.ULS, 0);
+            reinterpret_cast<double2 *>(a.rec + rec_UIN0(KS))[k] = inreg ? uin[0] : at(a.UIN, 0);
         }
     }
     agg[seg][kk] = bsum;
@@ -340,19 +384,21 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
 
     double2 w = win;
     if (ok) {
-#pragma unroll 4
-        for (int c = c0; c < c1; ++c) {
-            put(a.WIN, c, w);
-            const double2 wt = cfma(gam, at(a.UIN, c), at(a.WLS, c));
-            w = cfma(q, w, wt);
+        if (inreg) {
+#pragma unroll
+            for (int m = 0; m < CARRY_REG; ++m)
+                if (c0 + m < c1) {
+                    put(a.WIN, c0 + m, w);
+                    w = cfma(q, w, cfma(gam, uin[m], wls[m]));
+                }
+        } else {
+            for (int c = c0; c < c1; ++c) {
+                put(a.WIN, c, w);
+                w = cfma(q, w, cfma(gam, at(a.UIN, c), at(a.WLS, c)));
+            }
         }
     }
     if (seg == CARRY_SEG - 1 && ok) reinterpret_cast<double2 *>(a.rec + rec_AW(KS))[s * KS + k] = w;
-    if (blockIdx.x == 0 && s == 0 && threadIdx.x == 0) {
-        double d = 0;
-        for (int c = 0; c < Nc; ++c) d += a.dcpart[c];
-        a.rec[rec_DSUM(KS)] = d;
-    }
 }
 
 // ------------------------------------------------------------------------------------
