@@ -19,6 +19,7 @@
 namespace qg {
 
 constexpr int PCG_T = 256;
+constexpr int PCG_ROWB = 256;  // workgroups along y (rows strided)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -26,105 +27,166 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// block reduction of two values (one per system) -> partial[blockIdx][2]
-__device__ __forceinline__ void block_sum2(double a, double b, double *partial) {
-    __shared__ double sa[PCG_T / 64], sb[PCG_T / 64];
-    a = wave_sum(a);
-    b = wave_sum(b);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (lane == 0) {
-        sa[w] = a;
-        sb[w] = b;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        double ta = 0, tb = 0;
-        for (int k = 0; k < PCG_T / 64; ++k) {
-            ta += sa[k];
-            tb += sb[k];
-        }
-        const size_t blk = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-        partial[2 * blk] = ta;
-        partial[2 * blk + 1] = tb;
-    }
-}
-
 __device__ __forceinline__ bool is_pin(const PcgArgs &a, int64_t i, int64_t j) {
     return a.pinned0 && a.rank == 0 && i == 0 && j == 0;
 }
 
-// b = -(Pinv zeta), r = b, x = 0; partial ||b||^2
-__global__ __launch_bounds__(PCG_T) void pcg_rhs(PcgArgs a) {
-    const int64_t i = blockIdx.x * (int64_t)PCG_T + threadIdx.x, j = blockIdx.y;
-    double n0 = 0, n1 = 0;
-    if (i < a.M) {
-        const size_t o = fidx(i + 1, j + 1, a.ld);
-        const double z1 = a.in1[o], z2 = a.in2[o];
-        double b0 = -(a.proj_in[0] * z1 + a.proj_in[1] * z2);
-        const double b1 = -(a.proj_in[2] * z1 + a.proj_in[3] * z2);
-        if (is_pin(a, i, j)) b0 = 0;  // b[1] = 0 (model.jl:185)
-        a.r[0][o] = b0;
-        a.r[1][o] = b1;
-        a.x[0][o] = 0;
-        a.x[1][o] = 0;
-        n0 = b0 * b0;
-        n1 = b1 * b1;
-    }
-    block_sum2(n0, n1, a.partial);
-}
+// Grid: x = row segments of PCG_T points, y = PCG_ROWB workgroups striding over the rows,
+// so a reduction leaves (M / PCG_T) * PCG_ROWB partials, not one per row.
+#define PCG_FOR_POINTS(a)                                                                      \
+    const int64_t i = blockIdx.x * (int64_t)PCG_T + threadIdx.x;                               \
+    for (int64_t j = blockIdx.y; j < (a).P; j += gridDim.y)                                    \
+        if (i < (a).M)
 
-// q_s = B_s p_s (p carries a valid ghost ring); partial (p, q)
-__global__ __launch_bounds__(PCG_T) void pcg_apply(PcgArgs a) {
-    const int64_t i = blockIdx.x * (int64_t)PCG_T + threadIdx.x, j = blockIdx.y;
-    double d0 = 0, d1 = 0;
-    if (i < a.M) {
-        const int64_t ld = a.ld, mi = i + 1, mj = j + 1;
-        for (int s = 0; s < 2; ++s) {
-            const double *p = a.p[s];
-            const bool pinsys = (s == 0) && a.pinned0;
-            auto val = [&](int64_t di, int64_t dj) {
-                // the pinned unknown (global interior (0,0)) enters no other row: its column
-                // of the matrix is zeroed (laplacian.jl:71-73); checked in global coordinates
-                // because the neighbour of rank G-1's last row wraps onto rank 0
-                if (pinsys) {
-                    const int64_t gi = ((i + di) % a.M + a.M) % a.M;
-                    const int64_t gj = ((j + dj + a.j_offset) % a.P_total + a.P_total) % a.P_total;
-                    if (gi == 0 && gj == 0) return 0.0;
-                }
-                return p[fidx(mi + di, mj + dj, ld)];
-            };
-            double q;
-            if (is_pin(a, i, j) && pinsys) {
-                q = p[fidx(mi, mj, ld)];  // identity row
-            } else {
-                const double lap = ((((val(-1, 0) + val(1, 0)) - 4 * val(0, 0)) + val(0, -1)) + val(0, 1)) * a.idx2;
-                q = -(lap + a.alpha[s] * val(0, 0));
-            }
-            a.q[s][fidx(mi, mj, ld)] = q;
-            const double pv = p[fidx(mi, mj, ld)];
-            if (s == 0) d0 = pv * q;
-            else d1 = pv * q;
+// (B_s p)(i, j) for one interior point: -(5-point Laplacian + alpha_s) p, with the pinned
+// Poisson unknown (global interior (0,0), on rank 0) entering no other row -- its column of
+// the matrix is zeroed (laplacian.jl:71-73) -- and an identity row of its own.  The pin's
+// four neighbours are found in global coordinates: (1,0), (M-1,0), (0,1), (0,P_total-1)
+// (the last wraps onto rank G-1's top row).  p carries a valid ghost ring.
+__device__ __forceinline__ double apply_at(const PcgArgs &a, int s, const double *p, int64_t i, int64_t j) {
+    const int64_t ld = a.ld;
+    const double *c = p + fidx(i + 1, j + 1, ld);
+    double w = c[-1], e = c[1], so = c[-ld], n = c[ld];
+    if (s == 0 && a.pinned0) {
+        const int64_t jg = j + a.j_offset;
+        if (jg == 0) {
+            if (i == 0) return c[0];  // identity row
+            if (i == 1) w = 0;
+            if (i == a.M - 1) e = 0;
+        }
+        if (i == 0) {
+            if (jg == 1) so = 0;
+            if (jg == a.P_total - 1) n = 0;
         }
     }
-    block_sum2(d0, d1, a.partial);
+    const double lap = ((((w + e) - 4 * c[0]) + so) + n) * a.idx2;
+    return -(lap + a.alpha[s] * c[0]);
+}
+
+// right-hand side b_s = -(proj_in zeta)_s at one point, b = 0 on the pin row (model.jl:185)
+__device__ __forceinline__ double rhs_at(const PcgArgs &a, int s, int64_t i, int64_t j) {
+    const size_t o = fidx(i + 1, j + 1, a.ld);
+    const double z1 = a.in1[o], z2 = a.in2[o];
+    if (s == 0 && is_pin(a, i, j)) return 0.0;
+    return -(a.proj_in[2 * s] * z1 + a.proj_in[2 * s + 1] * z2);
+}
+
+template <int NV>
+__device__ __forceinline__ void block_sumN(const double (&v)[NV], double *partial) {
+    __shared__ double sv[NV][PCG_T / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+        const double t = wave_sum(v[k]);
+        if (lane == 0) sv[k][w] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const size_t blk = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+            double t = 0;
+            for (int g = 0; g < PCG_T / 64; ++g) t += sv[k][g];
+            partial[NV * blk + k] = t;
+        }
+    }
+}
+
+// b = -(Pinv zeta), r = b, x = 0; partial ||b||^2
+__global__ __launch_bounds__(PCG_T) void pcg_rhs(PcgArgs a) {
+    double v[2] = {0, 0};
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        for (int s = 0; s < 2; ++s) {
+            const double b = rhs_at(a, s, i, j);
+            a.r[s][o] = b;
+            a.x[s][o] = 0;
+            v[s] += b * b;
+        }
+    }
+    block_sumN<2>(v, a.partial);
+}
+
+// q_s = B_s p_s; partial (p, q)
+__global__ __launch_bounds__(PCG_T) void pcg_apply(PcgArgs a) {
+    double v[2] = {0, 0};
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        for (int s = 0; s < 2; ++s) {
+            const double q = apply_at(a, s, a.p[s], i, j);
+            a.q[s][o] = q;
+            v[s] += a.p[s][o] * q;
+        }
+    }
+    block_sumN<2>(v, a.partial);
+}
+
+// ---- fast path for the (exact) spectral preconditioner ---------------------------------
+// Iteration 1 of PCG from x0 = 0 with z0 = M^-1 b computed straight from zeta, fused:
+//   pcg_fast_dots:   (b, z0), (z0, B z0), (b, b) per system      -> alpha = (b,z0)/(z0,Bz0)
+//   pcg_fast_finish: r1 = b - alpha B z0 -> ||r1||^2;  psi = proj_out (alpha z0) with ghosts
+// (B z0 is recomputed instead of stored; the stencil is cheap, the bytes are not).
+__global__ __launch_bounds__(PCG_T) void pcg_fast_dots(PcgArgs a) {
+    double v[6] = {0, 0, 0, 0, 0, 0};  // per system: (b,z), (z,Bz), (b,b)
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        for (int s = 0; s < 2; ++s) {
+            const double b = rhs_at(a, s, i, j), z = a.z[s][o], q = apply_at(a, s, a.z[s], i, j);
+            v[3 * s] += b * z;
+            v[3 * s + 1] += z * q;
+            v[3 * s + 2] += b * b;
+        }
+    }
+    block_sumN<6>(v, a.partial);
+}
+
+__global__ __launch_bounds__(PCG_T) void pcg_fast_finish(PcgArgs a) {
+    double v[2] = {0, 0};
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        double x[2];
+        for (int s = 0; s < 2; ++s) {
+            const double al = a.scal[PCG_ALPHA + s];
+            const double r = rhs_at(a, s, i, j) - al * apply_at(a, s, a.z[s], i, j);
+            v[s] += r * r;
+            x[s] = al * a.z[s][o];
+        }
+        store_with_ghosts(a.out1, a.ld, a.M, a.P, i, j, a.proj_out[0] * x[0] + a.proj_out[1] * x[1], a.ghost_rows);
+        if (a.out2)
+            store_with_ghosts(a.out2, a.ld, a.M, a.P, i, j, a.proj_out[2] * x[0] + a.proj_out[3] * x[1],
+                              a.ghost_rows);
+    }
+    block_sumN<2>(v, a.partial);
+}
+
+// fallback after a fast iteration that did not converge: the general loop's state after
+// iteration 1 (x1 = alpha z0, r1 = b - alpha B z0, p0 = z0 with its ghost ring)
+__global__ __launch_bounds__(PCG_T) void pcg_fast_materialize(PcgArgs a) {
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        for (int s = 0; s < 2; ++s) {
+            const double al = a.scal[PCG_ALPHA + s];
+            a.x[s][o] = al * a.z[s][o];
+            a.r[s][o] = rhs_at(a, s, i, j) - al * apply_at(a, s, a.z[s], i, j);
+            store_with_ghosts(a.p[s], a.ld, a.M, a.P, i, j, a.z[s][o], a.ghost_rows);
+        }
+    }
 }
 
 // x += alpha p, r -= alpha q; partial ||r||^2
 __global__ __launch_bounds__(PCG_T) void pcg_update(PcgArgs a) {
-    const int64_t i = blockIdx.x * (int64_t)PCG_T + threadIdx.x, j = blockIdx.y;
-    double n0 = 0, n1 = 0;
-    if (i < a.M) {
+    double v[2] = {0, 0};
+    PCG_FOR_POINTS(a) {
         const size_t o = fidx(i + 1, j + 1, a.ld);
         for (int s = 0; s < 2; ++s) {
             const double al = a.scal[PCG_ALPHA + s];
             a.x[s][o] += al * a.p[s][o];
             const double rv = a.r[s][o] - al * a.q[s][o];
             a.r[s][o] = rv;
-            if (s == 0) n0 = rv * rv;
-            else n1 = rv * rv;
+            v[s] += rv * rv;
         }
     }
-    block_sum2(n0, n1, a.partial);
+    block_sumN<2>(v, a.partial);
 }
 
 // partial (r, z).  The spectral preconditioner inverts the pinned operator on every row but
@@ -132,36 +194,36 @@ __global__ __launch_bounds__(PCG_T) void pcg_update(PcgArgs a) {
 // completing the inverse there (z = r on that row) lets PCG remove the pin-row residual that
 // roundoff in the pin subtraction leaves in x.
 __global__ __launch_bounds__(PCG_T) void pcg_dot_rz(PcgArgs a) {
-    const int64_t i = blockIdx.x * (int64_t)PCG_T + threadIdx.x, j = blockIdx.y;
-    double d0 = 0, d1 = 0;
-    if (i < a.M) {
+    double v[2] = {0, 0};
+    PCG_FOR_POINTS(a) {
         const size_t o = fidx(i + 1, j + 1, a.ld);
         if (is_pin(a, i, j)) a.z[0][o] = a.r[0][o];
-        d0 = a.r[0][o] * a.z[0][o];
-        d1 = a.r[1][o] * a.z[1][o];
+        v[0] += a.r[0][o] * a.z[0][o];
+        v[1] += a.r[1][o] * a.z[1][o];
     }
-    block_sum2(d0, d1, a.partial);
+    block_sumN<2>(v, a.partial);
 }
 
 // p = z + beta p (first iteration: p = z), with the ghost ring (rows too when single-GPU)
 __global__ __launch_bounds__(PCG_T) void pcg_pupdate(PcgArgs a, int first) {
-    const int64_t i = blockIdx.x * (int64_t)PCG_T + threadIdx.x, j = blockIdx.y;
-    if (i >= a.M) return;
-    const size_t o = fidx(i + 1, j + 1, a.ld);
-    for (int s = 0; s < 2; ++s) {
-        const double v = first ? a.z[s][o] : a.z[s][o] + a.scal[PCG_BETA + s] * a.p[s][o];
-        store_with_ghosts(a.p[s], a.ld, a.M, a.P, i, j, v, a.ghost_rows);
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        for (int s = 0; s < 2; ++s) {
+            const double v = first ? a.z[s][o] : a.z[s][o] + a.scal[PCG_BETA + s] * a.p[s][o];
+            store_with_ghosts(a.p[s], a.ld, a.M, a.P, i, j, v, a.ghost_rows);
+        }
     }
 }
 
 // back-projection psi_l = P_fwd[l] . (x0, x1) with the ghost ring
 __global__ __launch_bounds__(PCG_T) void pcg_backproj(PcgArgs a) {
-    const int64_t i = blockIdx.x * (int64_t)PCG_T + threadIdx.x, j = blockIdx.y;
-    if (i >= a.M) return;
-    const size_t o = fidx(i + 1, j + 1, a.ld);
-    const double x0 = a.x[0][o], x1 = a.x[1][o];
-    store_with_ghosts(a.out1, a.ld, a.M, a.P, i, j, a.proj_out[0] * x0 + a.proj_out[1] * x1, a.ghost_rows);
-    if (a.out2) store_with_ghosts(a.out2, a.ld, a.M, a.P, i, j, a.proj_out[2] * x0 + a.proj_out[3] * x1, a.ghost_rows);
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        const double x0 = a.x[0][o], x1 = a.x[1][o];
+        store_with_ghosts(a.out1, a.ld, a.M, a.P, i, j, a.proj_out[0] * x0 + a.proj_out[1] * x1, a.ghost_rows);
+        if (a.out2)
+            store_with_ghosts(a.out2, a.ld, a.M, a.P, i, j, a.proj_out[2] * x0 + a.proj_out[3] * x1, a.ghost_rows);
+    }
 }
 
 // sum the per-block partials (fixed order) -> rank sums in scal[RSUM + 0/1]
@@ -185,6 +247,52 @@ __global__ __launch_bounds__(1024) void pcg_rank_sum(PcgArgs a, int nblk) {
     if (threadIdx.x == 0) {
         a.scal[PCG_RSUM] = s0[0];
         a.scal[PCG_RSUM + 1] = s1[0];
+    }
+}
+
+// sum NV per-block partials (fixed order) -> scal[PCG_RSUM6 ..)
+template <int NV>
+__global__ __launch_bounds__(1024) void pcg_rank_sumN(PcgArgs a, int nblk) {
+    __shared__ double sm[NV][1024];
+    double t[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) t[k] = 0;
+    for (int b = threadIdx.x; b < nblk; b += 1024)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) t[k] += a.partial[NV * b + k];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) sm[k][threadIdx.x] = t[k];
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (threadIdx.x < o)
+#pragma unroll
+            for (int k = 0; k < NV; ++k) sm[k][threadIdx.x] += sm[k][threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x < NV) a.scal[PCG_RSUM6 + threadIdx.x] = sm[threadIdx.x][0];
+}
+
+// fast-path scalars from the (gathered) sums: what 0: (b,z),(z,Bz),(b,b) -> alpha, rz, bb;
+// what 1: ||r1||^2 -> rr
+__global__ void pcg_fast_scalar(PcgArgs a, int what, const double *gathered, int nv, int nranks) {
+    if (threadIdx.x != 0) return;
+    for (int s = 0; s < 2; ++s) {
+        double *sc = a.scal;
+        if (what == 0) {
+            double bz = 0, zq = 0, bb = 0;
+            for (int g = 0; g < nranks; ++g) {
+                bz += gathered[nv * g + 3 * s];
+                zq += gathered[nv * g + 3 * s + 1];
+                bb += gathered[nv * g + 3 * s + 2];
+            }
+            sc[PCG_ALPHA + s] = (zq != 0 && bz != 0) ? bz / zq : 0.0;
+            sc[PCG_RZ + s] = bz;
+            sc[PCG_BB + s] = bb;
+        } else {
+            double rr = 0;
+            for (int g = 0; g < nranks; ++g) rr += gathered[nv * g + s];
+            sc[PCG_RR + s] = rr;
+        }
     }
 }
 
@@ -239,8 +347,8 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
         QG_CHECK(pre_.init(M, P, P_total, rank, nranks, dx, alpha, pinned0, neg, id, chunk_rows));
     }
     const size_t F = (size_t)(M + 2) * (size_t)(P + 2);
-    nblk_ = (int)(((M + PCG_T - 1) / PCG_T) * P);
-    const size_t bytes = sizeof(double) * (10 * F + 2 * (size_t)nblk_ + 64 + 2 * (size_t)nranks);
+    nblk_ = (int)(((M + PCG_T - 1) / PCG_T) * std::min<int64_t>(P, PCG_ROWB));
+    const size_t bytes = sizeof(double) * (10 * F + 6 * (size_t)nblk_ + 64 + 6 * (size_t)nranks);
     if (hipMalloc(&mem_, bytes) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -255,7 +363,7 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
         a.z[s] = m + (8 + s) * F;
     }
     a.partial = m + 10 * F;
-    a.scal = a.partial + 2 * (size_t)nblk_;
+    a.scal = a.partial + 6 * (size_t)nblk_;
     gathered_ = a.scal + 64;
     return QG_OK;
 }
@@ -277,6 +385,24 @@ int PcgSolver::reduce(int what, hipStream_t s, SpectralSolver::GatherFn gather, 
     return QG_OK;
 }
 
+// fast-path reductions: NV partials per block -> rank sums -> (all-gather) -> scalars
+template <int NV>
+static int reduce_fast(PcgArgs &a, int nblk, int what, double *gathered, hipStream_t s,
+                       SpectralSolver::GatherFn gather, void *user) {
+    pcg_rank_sumN<NV><<<1, 1024, 0, s>>>(a, nblk);
+    QG_LAUNCH_CHECK();
+    const double *src = a.scal + PCG_RSUM6;
+    int nranks = 1;
+    if (gather) {
+        QG_CHECK(gather(user, a.scal + PCG_RSUM6, gathered, NV, s));
+        src = gathered;
+        nranks = a.nranks;
+    }
+    pcg_fast_scalar<<<1, 64, 0, s>>>(a, what, src, NV, nranks);
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
 int PcgSolver::solve(const double *in1, const double *in2, double *out1, double *out2, int ghost_rows,
                      hipStream_t s, SpectralSolver::GatherFn gather, void *user, HaloFn halo, void *halo_user) {
     if (!mem_) return QG_ERR_NOT_BOUND;
@@ -286,7 +412,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
     a.out1 = out1;
     a.out2 = out2;
     a.ghost_rows = ghost_rows;
-    const dim3 grid((unsigned)((a.M + PCG_T - 1) / PCG_T), (unsigned)a.P);
+    const dim3 grid((unsigned)((a.M + PCG_T - 1) / PCG_T), (unsigned)std::min<int64_t>(a.P, PCG_ROWB));
     auto precond = [&]() -> int {
         if (precond_ == QG_PRECOND_SPECTRAL) {
             QG_CHECK(pre_.solve(a.r[0], a.r[1], a.z[0], a.z[1], ghost_rows, s, gather, user));
@@ -304,26 +430,70 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         }
         return QG_OK;
     };
-    pcg_rhs<<<grid, PCG_T, 0, s>>>(a);
-    QG_LAUNCH_CHECK();
-    QG_CHECK(reduce(0, s, gather, user));
-    QG_CHECK(precond());
-    pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
-    QG_LAUNCH_CHECK();
-    QG_CHECK(reduce(4, s, gather, user));
-    pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 1);
-    QG_LAUNCH_CHECK();
-    QG_CHECK(fix_p_ghosts());
     double host[PCG_NSCAL];
     iters_ = 0;
     relres_[0] = relres_[1] = -1;
     int status = QG_ERR_NOT_CONVERGED;
+    bool resume = false;  // continue the general loop after a fast first iteration
+    if (precond_ == QG_PRECOND_SPECTRAL) {
+        // z0 = B^-1 b straight from zeta: B^-1 (-proj_in zeta) = A^-1 proj_in zeta, i.e. the
+        // spectral solve with the model's projection (the pin row of b is irrelevant to it)
+        const double id[4] = {1, 0, 0, 1};
+        QG_CHECK(pre_.solve(a.in1, a.in2, a.z[0], a.z[1], ghost_rows, s, gather, user, a.proj_in, id));
+        if (!ghost_rows && halo) {
+            double *f[2] = {a.z[0], a.z[1]};
+            QG_CHECK(halo(halo_user, f, 2, a.M, a.P, -1, nullptr, s));
+        }
+        pcg_fast_dots<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce_fast<6>(a, nblk_, 0, gathered_, s, gather, user));
+        pcg_fast_finish<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce_fast<2>(a, nblk_, 1, gathered_, s, gather, user));
+        QG_HIP(hipMemcpyAsync(host, a.scal, sizeof(host), hipMemcpyDeviceToHost, s));
+        QG_HIP(hipStreamSynchronize(s));
+        iters_ = 1;
+        bool done = true;
+        for (int k = 0; k < 2; ++k) {
+            const double bb = host[PCG_BB + k], rr = host[PCG_RR + k];
+            relres_[k] = bb > 0 ? std::sqrt(rr / bb) : std::sqrt(rr);
+            if (!(relres_[k] <= rtol_)) done = false;
+        }
+        if (done) return QG_OK;  // psi already written by pcg_fast_finish
+        pcg_fast_materialize<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(fix_p_ghosts());
+        resume = true;
+    } else {
+        pcg_rhs<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce(0, s, gather, user));
+        QG_CHECK(precond());
+        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce(4, s, gather, user));
+        pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 1);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(fix_p_ghosts());
+    }
     // roundoff floor: ||B e|| / ||b|| >= ~cond(B) eps, so a target below it is never met.  Stop
     // once the residual has stagnated (less than 2x decrease over 3 iterations) at or below
     // 1e-10 -- the iterate is then as accurate as the arithmetic allows.
     double prev[2] = {1e300, 1e300};
     int stall = 0;
-    for (int it = 1; it <= maxit_; ++it) {
+    for (int it = resume ? 2 : 1; it <= maxit_; ++it) {
+        if (resume) {  // z1 = M^-1 r1, beta, p1 = z1 + beta p0 (the tail of iteration 1)
+            resume = false;
+            prev[0] = relres_[0];
+            prev[1] = relres_[1];
+            QG_CHECK(precond());
+            pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
+            QG_LAUNCH_CHECK();
+            QG_CHECK(reduce(3, s, gather, user));
+            pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 0);
+            QG_LAUNCH_CHECK();
+            QG_CHECK(fix_p_ghosts());
+        }
         pcg_apply<<<grid, PCG_T, 0, s>>>(a);
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce(1, s, gather, user));

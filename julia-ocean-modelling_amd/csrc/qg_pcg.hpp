@@ -7,7 +7,7 @@
 namespace qg {
 
 // device scalar slots (per system s: +s)
-enum { PCG_BB = 0, PCG_RZ = 2, PCG_ALPHA = 4, PCG_BETA = 6, PCG_RR = 8, PCG_RSUM = 10, PCG_NSCAL = 12 };
+enum { PCG_BB = 0, PCG_RZ = 2, PCG_ALPHA = 4, PCG_BETA = 6, PCG_RR = 8, PCG_RSUM = 10, PCG_RSUM6 = 12, PCG_NSCAL = 18 };
 
 struct PcgArgs {
     int64_t M, P, ld, P_total, j_offset;
@@ -20,7 +20,7 @@ struct PcgArgs {
     const double *in1, *in2;
     double *out1, *out2;
     double *x[2], *r[2], *p[2], *q[2], *z[2];  // (M+2, P+2) fields
-    double *partial;                            // [blocks][2]
+    double *partial;                            // [blocks][2] (fast path: [blocks][6])
     double *scal;                               // PCG_NSCAL doubles
 };
 

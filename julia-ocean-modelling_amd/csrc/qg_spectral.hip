@@ -831,9 +831,11 @@ SpectralSolver::~SpectralSolver() {
 }
 
 int SpectralSolver::solve(const double *in1, const double *in2, double *out1, double *out2, int write_ghost_rows,
-                          hipStream_t s, GatherFn gather, void *user) {
+                          hipStream_t s, GatherFn gather, void *user, const double *pin_in, const double *pin_out) {
     if (!mem_) return QG_ERR_NOT_BOUND;
     SpecArgs a = a_;
+    if (pin_in) std::memcpy(a.pin_in, pin_in, sizeof(a.pin_in));
+    if (pin_out) std::memcpy(a.pin_out, pin_out, sizeof(a.pin_out));
     a.in1 = in1;
     a.in2 = in2 ? in2 : in1;
     a.out1 = out1;

@@ -80,7 +80,8 @@ public:
     // enqueue the whole solve; `gather` (may be null) all-gathers rec -> grec across ranks
     typedef int (*GatherFn)(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
     int solve(const double *in1, const double *in2, double *out1, double *out2, int write_ghost_rows,
-              hipStream_t s, GatherFn gather = nullptr, void *user = nullptr);
+              hipStream_t s, GatherFn gather = nullptr, void *user = nullptr, const double *pin_in = nullptr,
+              const double *pin_out = nullptr);  // optional per-call projections
     const SpecArgs &args() const { return a_; }
     size_t device_bytes() const { return bytes_; }
 
