@@ -97,3 +97,33 @@ def test_run_model_metadata_and_log_cpu():
     qgamd.log_model_params(m, lines.append)
     assert lines[0] == "Parameters:" and lines[-1] == "Total steps = 840960\n"
     assert lines[8:10] == ["M = 512", "P = 256"]
+
+
+def test_invalid_parameters_refused_without_touching_the_gpu(qglib):
+    """qg_create validates before any device call: bad sizes / non-positive dx and the
+    reference's sign condition on beta_1, beta_2 (model.jl:38) return QG_ERR_INVALID_ARG;
+    NULL handles are refused by every entry point."""
+    import qgamd._lib as L
+    import qgamd
+
+    def params(**kw):
+        p = L.QgParams()
+        qglib.qg_default_params(C.byref(p))
+        m = qgamd.bench_model(32)
+        for f in ("H_1", "H_2", "beta", "Lx", "Ly", "dt", "T", "U", "M", "P", "dx", "visc", "r", "R_d",
+                  "initial_kick"):
+            setattr(p, f, getattr(m, f))
+        for k, v in kw.items():
+            setattr(p, k, v)
+        return p
+
+    ctx = C.c_void_p()
+    for bad in ({"M": 1}, {"P": 0}, {"dx": 0.0}, {"R_d": -1.0}, {"solver": 7}):
+        p = params(**bad)
+        assert qglib.qg_create(C.byref(p), 0, None, C.byref(ctx)) == -1, bad
+    p = params(U=0.01)  # beta_1 = beta + S1 U and beta_2 = beta - S2 U both positive
+    assert qglib.qg_create(C.byref(p), 0, None, C.byref(ctx)) == -1
+    assert qglib.qg_evolve_zeta(None, 1) == -1
+    assert qglib.qg_evolve_psi(None) == -1
+    assert qglib.qg_step(None, 1) == -1
+    assert qglib.qg_destroy(None) == 0

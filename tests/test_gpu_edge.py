@@ -1,0 +1,62 @@
+"""Edge cases of the device path against the C oracle: the smallest grids the spectral solver
+takes (M = 8, P = 2), odd P (chunk of one row), non-square slabs both ways, an explicit chunk
+size, and the refusal of what the spectral solver cannot do (non power-of-two M), which PCG
+without preconditioner still solves.  Relative RMS < 1e-10 after a few Euler + AB3 steps."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+    from oracle import qg_oracle, qg_ref
+    qg_oracle.build()
+    return qgamd, qg_oracle, qg_ref
+
+
+@pytest.mark.parametrize("M,P,kw", [(8, 2, {}), (8, 3, {}), (16, 48, {}), (64, 16, {}), (16, 128, {}),
+                                    (32, 64, {"chunk_rows": 4}), (32, 60, {"chunk_rows": 0})])
+def test_small_and_ragged_grids(env, M, P, kw):
+    qg, O, R = env
+    steps = 5
+    st = qg.run_model_no_output(qg.bench_model(M, P=P), nsteps=steps, **kw)
+    ref = O.State(R.bench_model(M, P=P)).run(steps)
+    for n in ("psi", "zeta"):
+        assert rel(st.to_numpy(n), getattr(ref, n)) < TOL, (n, M, P)
+
+
+def test_chunk_size_does_not_change_the_answer(env):
+    qg, O, R = env
+    m = qg.bench_model(64)
+    a = qg.run_model_no_output(m, nsteps=4, chunk_rows=16).to_numpy("psi")
+    b = qg.run_model_no_output(m, nsteps=4, chunk_rows=2).to_numpy("psi")
+    assert rel(a, b) < 1e-12
+
+
+def test_non_power_of_two_rows(env):
+    qg, O, R = env
+    m = qg.bench_model(48, P=40)
+    with pytest.raises(qg.QGError) as e:  # the spectral solver needs M = 2^k
+        qg.State(m)
+    assert e.value.status == -2
+    st = qg.run_model_no_output(m, nsteps=3, solver=1, precond=0, pcg_maxit=2000)
+    ref = O.State(R.bench_model(48, P=40)).run(3)
+    assert rel(st.to_numpy("psi"), ref.psi) < 1e-8  # plain CG, stagnation floor ~1e-10 relres
+
+
+def test_invalid_arguments_are_refused(env):
+    qg, O, R = env
+    st = qg.State(qg.bench_model(32))
+    with pytest.raises(qg.QGError) as e:
+        st.evolve_zeta_(0)  # timesteps are 1-based (model.jl:160)
+    assert e.value.status == -1

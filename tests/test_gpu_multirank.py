@@ -23,7 +23,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, M, P, steps, outdir):
+def _worker(rank, world, port, M, P, steps, outdir, solver=0):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
@@ -38,7 +38,7 @@ def _worker(rank, world, port, M, P, steps, outdir):
     from qgamd.hostcomm import TorchDistTransport
 
     m = qgamd.bench_model(M, P=P)
-    st = qgamd.State(m, P_local=P // world)
+    st = qgamd.State(m, P_local=P // world, solver=solver)
     TorchDistTransport().attach(st, world, rank)
     st.initialise()
     st.run(1, steps)
@@ -49,8 +49,11 @@ def _worker(rank, world, port, M, P, steps, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,M,P,steps", [(2, 64, 64, 6), (4, 32, 64, 5), (2, 128, 96, 4)])
-def test_slabs_match_single_gpu(world, M, P, steps):
+@pytest.mark.parametrize("world,M,P,steps,solver", [(2, 64, 64, 6, 0), (4, 32, 64, 5, 0), (2, 128, 96, 4, 0),
+                                                     (2, 64, 64, 6, 1), (4, 32, 64, 4, 1)])
+def test_slabs_match_single_gpu(world, M, P, steps, solver):
+    """solver 0 = spectral (record all-gather), 1 = PCG with the spectral preconditioner
+    (its dot products and the z halo also cross the slabs)."""
     import torch
     import torch.multiprocessing as mp
 
@@ -58,13 +61,13 @@ def test_slabs_match_single_gpu(world, M, P, steps):
         pytest.skip("no GPU")
     import qgamd
 
-    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps)
+    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps, solver=solver)
     torch.cuda.synchronize()
     g = {n: ref.to_numpy(n) for n in ("zeta", "psi", "f_store")}
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver)) for r in range(world)]
         for p in procs:
             p.start()
         for p in procs:
