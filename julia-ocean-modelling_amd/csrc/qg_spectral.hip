@@ -26,7 +26,9 @@ struct Geo {
 #ifndef QG_SPEC_TDIV
 #define QG_SPEC_TDIV 8
 #endif
-    static constexpr int T = N / QG_SPEC_TDIV < 64 ? 64 : (N / QG_SPEC_TDIV > 1024 ? 1024 : N / QG_SPEC_TDIV);
+    // (below N = 2048 the N/8 workgroup would be too small to keep a CU busy: N/4, <= 256)
+    static constexpr int T0 = N / QG_SPEC_TDIV >= 256 ? N / QG_SPEC_TDIV : (N / 4 < 256 ? N / 4 : 256);
+    static constexpr int T = T0 < 64 ? 64 : (T0 > 1024 ? 1024 : T0);
     static constexpr int MINW = T / 256 < 1 ? 1 : T / 256;
     static constexpr int KH = N / 2 + 1;
     // wavenumber slots per thread over k in [0, N/2); the real Nyquist line k = N/2 rides in
@@ -698,9 +700,13 @@ bool SpectralSolver::supports(int64_t M, int64_t P) {
     return M >= 8 && M <= 4096 && (M & (M - 1)) == 0 && P >= 2;
 }
 
+// Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic), small
+// enough that the P / L workgroups of passes A and B cover the 256 CUs, and dividing P.
 static int pick_chunk(int64_t P, int req) {
     if (req > 0) return (P % req == 0) ? req : -1;
-    for (int L = 16; L >= 1; L >>= 1)
+    int cap = 16;
+    while (cap > 1 && P / cap < 256) cap >>= 1;
+    for (int L = cap; L >= 1; L >>= 1)
         if (P % L == 0) return L;
     return 1;
 }

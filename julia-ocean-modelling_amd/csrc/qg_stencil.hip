@@ -362,7 +362,15 @@ int launch_tendency(const TendArgs &a, hipStream_t s) {
         case 5: return launch_tend_variant<512, 1>(a, 64, s);
         case 6: return launch_tend_variant<128, 2>(a, 64, s);
         case 7: return launch_tend_variant<256, 3>(a, 64, s);
-        default: return launch_tend_variant<256, 1>(a, 64, s);
+        default: {
+            // rows per strip: 64 when the grid is large enough to fill the chip with 2048+
+            // workgroups, fewer (down to 4) on small grids, where the serial row march and not
+            // HBM bandwidth sets the time
+            const int64_t nx = (a.M + 255) / 256, rows_total = (a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0);
+            int rows = 64;
+            while (rows > 4 && nx * 2 * ((rows_total + rows - 1) / rows) < 2048) rows >>= 1;
+            return launch_tend_variant<256, 1>(a, rows, s);
+        }
     }
 }
 
