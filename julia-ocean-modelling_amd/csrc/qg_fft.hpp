@@ -7,6 +7,9 @@
 // registers, in exactly the element order of a coalesced row access (element t + r*T), so the
 // caller's global load / store feeds the transform without an LDS round trip.
 //
+// When two row buffers do not fit in LDS (N = 8192) the passes run in place on one buffer
+// with a barrier between each pass's reads and writes (callers pass b1 == b0).
+//
 // Twiddles live in LDS (row-invariant, filled once per workgroup from the global table
 // tw[m] = exp(-2 pi i m / N)): one small table per pass, entries exp(-2 pi i k / (NS R)),
 // k < NS; passes with NS > 256 use a two-level table (64 low + NS/64 high entries, one
@@ -108,6 +111,8 @@ struct Passes<N, T, NS, true> {
     static constexpr int count = 0, last_ns = 0, tw_here = 0, tw_total = 0;
 };
 
+constexpr int LDS_COMPLEX_MAX = 160 * 1024 / 16;  // double2 elements in a CU's 160 KB LDS
+
 template <int N, int T>
 struct FftPlan {
     using P = Passes<N, T, 1>;
@@ -119,7 +124,10 @@ struct FftPlan {
     // one butterfly per thread in the first / last pass, in row order t + r*T
     static constexpr bool REG_IN = (N / R0 == T);
     static constexpr bool REG_OUT = (N / R_LAST == T);
-    static constexpr int LDS = 2 * LdsSize<N>::value + TW;  // complex elements
+    // two row buffers (ping-pong, one barrier per pass) when they fit, else one buffer
+    // transformed in place (two barriers per pass): N = 8192
+    static constexpr bool PINGPONG = 2 * LdsSize<N>::value + TW <= LDS_COMPLEX_MAX;
+    static constexpr int LDS = (PINGPONG ? 2 : 1) * LdsSize<N>::value + TW;  // complex elements
     template <int NS>
     static constexpr int tw_off() { return P::tw_total - Passes<N, T, NS>::tw_total; }
 };
@@ -189,6 +197,7 @@ __device__ __forceinline__ void fft_pass(const double2 *src, double2 *dst, const
 #pragma unroll
         for (int r = 0; r < R; ++r) io[r] = v[0][r];
     } else {
+        if constexpr (!FftPlan<N, T>::PINGPONG && !FROM_REG) __syncthreads();  // in place: reads first
 #pragma unroll
         for (int p = 0; p < PER; ++p) {
             const int j = t + p * T;
@@ -237,9 +246,9 @@ struct FftFromLds {
     using Plan = FftPlan<N, T>;
     // passes that write a buffer: all, or all but the last
     static constexpr int WRITES = Plan::NPASS - (OUT_REG ? 1 : 0);
-    static constexpr bool result_in_b1 = (WRITES % 2) == 1;
+    static constexpr bool result_in_b1 = Plan::PINGPONG && (WRITES % 2) == 1;
     // buffer read after the last barrier (by the last pass when OUT_REG, else by the caller)
-    static constexpr bool b0_read_late = OUT_REG ? (WRITES % 2 == 0) : !result_in_b1;
+    static constexpr bool b0_read_late = !Plan::PINGPONG || (OUT_REG ? (WRITES % 2 == 0) : !result_in_b1);
     __device__ static __forceinline__ void run(double2 *b0, double2 *b1, const double2 *twl,
                                                double2 (&io)[Plan::R_LAST]) {
         fft_run<N, T, 1, 0, INV, OUT_REG>(b0, b1, twl, opaque_tid(), io);
@@ -251,7 +260,7 @@ struct FftFromLds {
 template <int N, int T, bool INV>
 struct FftFromReg {
     using Plan = FftPlan<N, T>;
-    static constexpr bool result_in_b1 = (Plan::NPASS % 2) == 0;
+    static constexpr bool result_in_b1 = Plan::PINGPONG && (Plan::NPASS % 2) == 0;
     static constexpr bool b0_read_late = !result_in_b1;
     __device__ static __forceinline__ void run(double2 (&in)[Plan::R0], double2 *b0, double2 *b1,
                                                const double2 *twl) {

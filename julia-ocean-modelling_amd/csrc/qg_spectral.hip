@@ -27,6 +27,7 @@ struct Geo {
 #define QG_SPEC_TDIV 8
 #endif
     // (below N = 2048 the N/8 workgroup would be too small to keep a CU busy: N/4, <= 256)
+    // (N = 8192: 1024 threads, registers capped at 128 -- some spill; capability, not speed)
     static constexpr int T0 = N / QG_SPEC_TDIV >= 256 ? N / QG_SPEC_TDIV : (N / 4 < 256 ? N / 4 : 256);
     static constexpr int T = T0 < 64 ? 64 : (T0 > 1024 ? 1024 : T0);
     static constexpr int MINW = T / 256 < 1 ? 1 : T / 256;
@@ -54,7 +55,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     constexpr bool RES_B1 = Plan::REG_IN ? FwdReg::result_in_b1 : FwdLds::result_in_b1;
     constexpr bool B0_LATE = Plan::REG_IN ? FwdReg::b0_read_late : FwdLds::b0_read_late;
     extern __shared__ double2 lds[];
-    double2 *b0 = lds, *b1 = lds + LdsSize<N>::value, *twl = lds + 2 * LdsSize<N>::value;
+    double2 *b0 = lds, *b1 = Plan::PINGPONG ? lds + LdsSize<N>::value : lds,
+            *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
     const double2 *Zb = RES_B1 ? b1 : b0;
     fft_init_twiddles<N, T>(twl, a.tw);
     __syncthreads();
@@ -90,14 +92,16 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
             }
         }
     };
-    load_row(e);
+    constexpr bool PF = N < 8192;  // (N = 8192: no register prefetch, registers are short)
+    if constexpr (PF) load_row(e);
     for (int j = e; j >= s0; --j) {
+        if constexpr (!PF) load_row(j);
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
         if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
             double2 in[Plan::R0];
 #pragma unroll
             for (int p = 0; p < EP; ++p) in[p] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
-            if (j > s0) load_row(j - 1);
+            if (PF && j > s0) load_row(j - 1);
             FwdReg::run(in, b0, b1, twl);
         } else {
 #pragma unroll
@@ -105,7 +109,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                 const int i = t + p * T;
                 if (N % T == 0 || i < N) b0[i] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
             }
-            if (j > s0) load_row(j - 1);
+            if (PF && j > s0) load_row(j - 1);
             __syncthreads();
             double2 unused[Plan::R_LAST];
             FwdLds::run(b0, b1, twl, unused);
@@ -531,7 +535,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     using Plan = FftPlan<N, T>;
     using Inv = FftFromLds<N, T, true, Plan::REG_OUT>;
     extern __shared__ double2 lds[];
-    double2 *b0 = lds, *b1 = lds + LdsSize<N>::value, *twl = lds + 2 * LdsSize<N>::value;
+    double2 *b0 = lds, *b1 = Plan::PINGPONG ? lds + LdsSize<N>::value : lds,
+            *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
     const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
     fft_init_twiddles<N, T>(twl, a.tw);
     __syncthreads();
@@ -565,7 +570,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             }
         }
     };
-    load_u(s0);  // first row in flight while the chunk carries are computed
+    constexpr bool PF = N < 8192;  // (N = 8192: no register prefetch, registers are short)
+    if constexpr (PF) load_u(s0);  // first row in flight while the chunk carries are computed
     // per line: carried term cu = r^(e+1-j) u_in and forward-filter state w.  Slot (0, t = 0)
     // packs the real lines k = 0 (.x) and k = N/2 (.y).
     double2 cu[KQ][2], w[KQ][2];
@@ -590,12 +596,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         }
     }
     for (int j = s0; j <= e; ++j) {
+        if constexpr (!PF) load_u(j);
         double2 ucur[KQ][2];
 #pragma unroll
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
             for (int s = 0; s < 2; ++s) ucur[q][s] = upf[q][s];
-        if (j < e) load_u(j + 1);
+        if (PF && j < e) load_u(j + 1);
         // compiler memory barrier: re-read the (L1-resident) coefficients every row instead of
         // hoisting them into registers, which would spill at this occupancy
         asm volatile("" ::: "memory");
@@ -692,12 +699,13 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
         case 1024: return launch_pass<1024>(passB, a, s);
         case 2048: return launch_pass<2048>(passB, a, s);
         case 4096: return launch_pass<4096>(passB, a, s);
+        case 8192: return launch_pass<8192>(passB, a, s);
         default: return QG_ERR_UNSUPPORTED;
     }
 }
 
 bool SpectralSolver::supports(int64_t M, int64_t P) {
-    return M >= 8 && M <= 4096 && (M & (M - 1)) == 0 && P >= 2;
+    return M >= 8 && M <= 8192 && (M & (M - 1)) == 0 && P >= 2;
 }
 
 // Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic), small

@@ -60,3 +60,11 @@ def test_invalid_arguments_are_refused(env):
     with pytest.raises(qg.QGError) as e:
         st.evolve_zeta_(0)  # timesteps are 1-based (model.jl:160)
     assert e.value.status == -1
+
+
+def test_widest_rows_8192(env):
+    """M = 8192 (the widest row the spectral solver takes: one in-place LDS row buffer)."""
+    qg, O, R = env
+    st = qg.run_model_no_output(qg.bench_model(8192, P=32, dt=60.0), nsteps=3)
+    ref = O.State(R.bench_model(8192, P=32, dt=60.0)).run(3)
+    assert rel(st.to_numpy("psi"), ref.psi) < TOL
