@@ -28,12 +28,13 @@ for _p in (ROOT, PKG):
 
 METRIC = "model timesteps/sec at N×N per GPU; achieved HBM GB/s vs roofline, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-B = 8  # bytes per double
 
-# algorithmic HBM bytes per interior grid point (both layers / both systems), see DESIGN.md
-BYTES_TENDENCY_AB3 = 2 * 6 * B  # per layer: read zeta, psi, F(t-1), F(t-2); write zeta+, F
-BYTES_SOLVE = 4 * 2 * B         # pass A: read zeta1,2 write u(2); pass B: read u(2) write psi1,2
-BYTES_STEP = BYTES_TENDENCY_AB3 + BYTES_SOLVE
+# algorithmic HBM bytes per interior grid point (both layers / both systems) for element size
+# B (8 = F64, 4 = F32 state), see DESIGN.md
+def bytes_per_point(B):
+    tendency = 2 * 6 * B  # per layer: read zeta, psi, F(t-1), F(t-2); write zeta+, F
+    solve = 4 * 2 * B     # pass A: read zeta1,2 write u (~2 reals/pt); pass B: read u, write psi1,2
+    return tendency, solve, tendency + solve
 
 
 def parse():
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--solver", choices=("spectral", "pcg"), default="spectral",
                     help="streamfunction inversion: direct spectral (default) or matrix-free PCG "
                          "preconditioned by the spectral solve")
+    ap.add_argument("--dtype", choices=("f64", "f32"), default="f64",
+                    help="state precision: f64 (the reference's, default) or f32 (BASELINE config 5)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
@@ -119,7 +122,8 @@ def main():
     torch.cuda.synchronize()
     t_setup = time.perf_counter()
     solver = qgamd._lib.QG_SOLVER_PCG if args.solver == "pcg" else qgamd._lib.QG_SOLVER_SPECTRAL
-    st = qgamd.State(m, solver=solver, chunk_rows=args.chunk_rows, P_local=n)
+    tdtype = torch.float32 if args.dtype == "f32" else torch.float64
+    st = qgamd.State(m, solver=solver, chunk_rows=args.chunk_rows, P_local=n, dtype=tdtype)
     if world == 1 and args.comm_self:
         import ctypes as C
         buf = C.create_string_buffer(128)
@@ -179,6 +183,7 @@ def main():
         return
 
     pts = n * n
+    BYTES_TENDENCY_AB3, BYTES_SOLVE, BYTES_STEP = bytes_per_point(4 if args.dtype == "f32" else 8)
     ms = el * 1e3 / K
     tend_gbs = BYTES_TENDENCY_AB3 * pts / (tend_ms * 1e-3) / 1e9
     step_gbs = BYTES_STEP * pts / (ms * 1e-3) / 1e9
@@ -187,14 +192,14 @@ def main():
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))
-            if pj.get("n") == n:
+            if pj.get("n") == n and args.dtype == "f64" and args.solver == "spectral":
                 traffic = pj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
         "metric": METRIC,
         "value": world * K / el,
-        "unit": f"timesteps/s ({n}x{n} F64 slab-steps summed over GPUs)",
+        "unit": f"timesteps/s ({n}x{n} {args.dtype.upper()} slab-steps summed over GPUs)",
         "n_gpus": world,
         "steps": K,
         "warmup": args.warmup,
@@ -204,10 +209,11 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": args.dtype,
         "data": "synthetic: seeded counter-based noise initial conditions (model.jl:41-42 uses unseeded rand)",
         "config": {
-            "workload": f"2-layer Phillips {n}x{n} Float64 per GPU (BASELINE configs[2]), Arakawa "
+            "workload": f"2-layer Phillips {n}x{n} {'Float32' if args.dtype == 'f32' else 'Float64'} per GPU "
+                        f"({'BASELINE configs[4]' if args.dtype == 'f32' else 'BASELINE configs[2]'}), Arakawa "
                         "tendency + AB3, pinned Poisson + modified Helmholtz inversion, dt = "
                         f"{args.dt:g} s, bench params of julia_bench_parts.jl:6-18",
             "grid_per_gpu": [n, n],
@@ -234,7 +240,7 @@ def main():
             "algorithmic_bytes_per_step": BYTES_STEP * pts, "solve_ms": solve_ms, "tendency_ms": tend_ms,
         },
     }
-    if args.cpu_steps > 0 and world == 1:
+    if args.cpu_steps > 0 and world == 1 and args.dtype == "f64":
         out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads, args.cpu_steps_1t)
     else:
         out["cpu_baseline"] = None

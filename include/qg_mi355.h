@@ -14,7 +14,8 @@
  *   sp_solve_modified_helmholtz / sp_solve_poisson         src/schemes/laplacian.jl:78-111
  *
  * Conventions (identical to the reference's arrays):
- *   - every field is IEEE Float64, Julia column-major (M+2) x (P+2) with a one-cell ghost
+ *   - every field is IEEE Float64 (or Float32 with params.dtype = QG_F32, model state only),
+ *     Julia column-major (M+2) x (P+2) with a one-cell ghost
  *     ring: element (i, j) (0-based, ghosts included) lives at  ptr[i + (M+2)*j];
  *   - the model state zeta, psi, f_store are (M+2, P+2, 2, 3) arrays: layer l (0/1) and
  *     history slot s (0/1/2) of field X start at X + (M+2)*(P+2)*(l + 2*s);
@@ -48,7 +49,7 @@
 extern "C" {
 #endif
 
-#define QG_ABI_VERSION 1
+#define QG_ABI_VERSION 2
 
 typedef enum {
     QG_OK = 0,
@@ -65,6 +66,12 @@ typedef enum {
     QG_SOLVER_SPECTRAL = 0, /* direct: x-DFT + parallel cyclic tridiagonal solve in y     */
     QG_SOLVER_PCG = 1       /* matrix-free PCG on the 5-point operator                     */
 } qg_solver_kind;
+
+typedef enum {
+    QG_F64 = 0,             /* IEEE Float64 state: the reference's arithmetic              */
+    QG_F32 = 1              /* Float32 state (BASELINE config 5); transforms and y-solves  *
+                             * still run in F64, the fields and u are stored in F32         */
+} qg_dtype;
 
 typedef enum {
     QG_PRECOND_NONE = 0,    /* plain CG                                                    */
@@ -86,6 +93,9 @@ typedef struct qg_params {
                          * run that stagnates at its roundoff floor <= 1e-10 also stops */
     int32_t pcg_maxit;  /* default 500                                                  */
     int32_t chunk_rows; /* y-chunk of the spectral solver; 0 = automatic                */
+    int32_t dtype;      /* qg_dtype of the state arrays (default QG_F64; QG_F32 needs   *
+                         * QG_SOLVER_SPECTRAL)                                          */
+    int32_t reserved0;
 } qg_params;
 
 typedef struct qg_ctx qg_ctx;       /* one model instance (one rank) on one device       */
@@ -108,8 +118,9 @@ void qg_default_params(qg_params *p);
  * (model.jl:12-34, laplacian.jl:60-75, called at run_model_no_output.jl:5-6)        */
 int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out);
 int qg_destroy(qg_ctx *ctx);
-/* zeta, psi, f_store: device (M+2, P+2, 2, 3) Float64 arrays owned by the caller */
-int qg_bind_state(qg_ctx *ctx, double *zeta, double *psi, double *f_store);
+/* zeta, psi, f_store: device (M+2, P+2, 2, 3) arrays owned by the caller, of the element
+ * type params.dtype names (double for QG_F64, float for QG_F32) */
+int qg_bind_state(qg_ctx *ctx, void *zeta, void *psi, void *f_store);
 /* initialise_model (model.jl:37-62) on the device, seeded: psi_l interior (i, j) =
  * kick*U*Ly*u01(seed_l, i + M*j_global); zeroes all other slots and f_store; resets the
  * slot rotation. */
@@ -135,7 +146,7 @@ int qg_synchronize(qg_ctx *ctx);
  * moves the staging buffer to the caller's HOST buffers (page-locked memory gives an
  * asynchronous copy) while the caller keeps stepping.  A second qg_snapshot first waits for
  * the previous copy.  qg_snapshot_wait blocks until the host buffers are complete.          */
-int qg_snapshot(qg_ctx *ctx, double *host_zeta, double *host_psi);
+int qg_snapshot(qg_ctx *ctx, void *host_zeta, void *host_psi);  /* elements as params.dtype */
 int qg_snapshot_wait(qg_ctx *ctx);
 
 /* ---- multi-GPU (one rank per GPU, slab decomposition in y) ---------------------------

@@ -15,7 +15,7 @@ int comm_destroy(void *comm);
 int comm_allgather(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
 int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
               hipStream_t s);
-int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t M,
+int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t ld,
                   int64_t P, hipStream_t s, bool ghost_f2);
 int comm_init(void **comm, int nranks, int rank, const char id[128]);
 int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sendrecv_fn sr, void *user);
@@ -36,7 +36,8 @@ struct qg_ctx {
     Derived d{};
     int device = 0;
     hipStream_t stream = nullptr;
-    double *zeta = nullptr, *psi = nullptr, *fst = nullptr;
+    void *zeta = nullptr, *psi = nullptr, *fst = nullptr;  // element type: p.dtype
+    size_t esize = 8;                                     // sizeof(element)
     int heads[3] = {0, 0, 0};  // physical slot of logical slot 1 for zeta, psi, f_store
     bool initialised = false;
     int rank = 0, nranks = 1;
@@ -48,7 +49,7 @@ struct qg_ctx {
     // qg_canonicalize
     bool ghosts_pending = false;
     // snapshots: device staging buffer [zeta 2 layers | psi 2 layers], copy stream + events
-    double *snap = nullptr;
+    char *snap = nullptr;
     hipStream_t snap_stream = nullptr;
     hipEvent_t snap_ready = nullptr, snap_done = nullptr;
     bool snap_inflight = false;
@@ -57,7 +58,13 @@ struct qg_ctx {
     int last_status = QG_OK;  // of the last solve (PCG: QG_ERR_NOT_CONVERGED is kept here)
     size_t F = 0;  // doubles per (M+2, P+2) field
 
-    double *field(double *base, int layer, int slot) const { return base + F * (size_t)(layer + 2 * slot); }
+    void *fieldv(void *base, int layer, int slot) const {
+        return static_cast<char *>(base) + esize * F * (size_t)(layer + 2 * slot);
+    }
+    double *field(void *base, int layer, int slot) const { return static_cast<double *>(fieldv(base, layer, slot)); }
+    template <class T>
+    T *fieldt(void *base, int layer, int slot) const { return static_cast<T *>(fieldv(base, layer, slot)); }
+    int64_t row_words() const { return (int64_t)((p.M + 2) * esize / 8); }  // a row, in 8-byte words
 };
 
 extern "C" {
@@ -97,6 +104,8 @@ static int check_params(const qg_params *p) {
     if (p->M < 2 || p->P < 2 || !(p->dx > 0) || !(p->H_1 > 0) || !(p->H_2 > 0) || !(p->R_d > 0))
         return QG_ERR_INVALID_ARG;
     if (p->solver != QG_SOLVER_SPECTRAL && p->solver != QG_SOLVER_PCG) return QG_ERR_INVALID_ARG;
+    if (p->dtype != QG_F64 && p->dtype != QG_F32) return QG_ERR_INVALID_ARG;
+    if (p->dtype == QG_F32 && (p->solver != QG_SOLVER_SPECTRAL || (p->M % 2) != 0)) return QG_ERR_UNSUPPORTED;
     return QG_OK;
 }
 
@@ -116,7 +125,7 @@ static int build_solver(qg_ctx *c) {
     if (!SpectralSolver::supports(p.M, p.P)) return QG_ERR_UNSUPPORTED;
     auto s = std::make_unique<SpectralSolver>();
     QG_CHECK(s->init(p.M, p.P, p.P * c->nranks, c->rank, c->nranks, p.dx, alpha, 1, c->d.Pinv, p.P_fwd,
-                     p.chunk_rows));
+                     p.chunk_rows, p.dtype == QG_F32));
     c->spec = std::move(s);
     return QG_OK;
 }
@@ -132,6 +141,7 @@ int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out) {
     c->device = device;
     c->stream = static_cast<hipStream_t>(stream);
     c->F = (size_t)(p->M + 2) * (size_t)(p->P + 2);
+    c->esize = p->dtype == QG_F32 ? sizeof(float) : sizeof(double);
     // beta_1 and beta_2 must have opposite signs (model.jl:38)
     if (!((c->d.beta1 > 0 && c->d.beta2 < 0) || (c->d.beta1 < 0 && c->d.beta2 > 0))) {
         delete c;
@@ -160,7 +170,7 @@ int qg_destroy(qg_ctx *c) {
     return QG_OK;
 }
 
-int qg_bind_state(qg_ctx *c, double *zeta, double *psi, double *f_store) {
+int qg_bind_state(qg_ctx *c, void *zeta, void *psi, void *f_store) {
     if (!c || !zeta || !psi || !f_store) return QG_ERR_INVALID_ARG;
     c->zeta = zeta;
     c->psi = psi;
@@ -176,7 +186,7 @@ int qg_initialise(qg_ctx *c, uint64_t seed1, uint64_t seed2) {
     const qg_params &p = c->p;
     QG_HIP(hipSetDevice(c->device));
     const double amp = p.initial_kick * p.U * p.Ly;
-    QG_CHECK(launch_initialise_global(c->zeta, c->psi, c->fst, p.M, p.P, p.P * c->nranks,
+    QG_CHECK(launch_initialise_global(c->zeta, c->psi, c->fst, (int)c->esize, p.M, p.P, p.P * c->nranks,
                                       (int64_t)c->rank * p.P, amp, c->d.S1, c->d.S2, p.dx, seed1, seed2,
                                       c->stream));
     c->heads[0] = c->heads[1] = c->heads[2] = 0;
@@ -198,12 +208,15 @@ int qg_set_slots(qg_ctx *c, const int heads[3]) {
     return QG_OK;
 }
 
-static void fill_wrap_rows(const qg_ctx *c, const double *base, RowSrc &rs) {
+extern "C++" {
+template <class T>
+static void fill_wrap_rows(const qg_ctx *c, const T *base, RowSrcT<T> &rs) {
     // single-GPU: rows -2,-1,P,P+1 are the periodic images P-2,P-1,0,1
     const int64_t P = c->p.P, ld = c->p.M + 2;
     const int64_t rows[4] = {(P - 2 + P) % P, P - 1, 0, 1 % P};
     for (int h = 0; h < 4; ++h) rs.halo[h] = base + fidx(1, rows[h] + 1, ld);
 }
+}  // extern "C++"
 
 // ---- multi-GPU ghost rows --------------------------------------------------------------
 // the newest zeta, psi and F (both layers): the fields whose ghost rows a step leaves stale
@@ -220,19 +233,18 @@ static int flush_ghosts(qg_ctx *c) {
     if (!c->distributed || !c->ghosts_pending) return QG_OK;
     double *f[6];
     const int n = newest_fields(c, f);
-    QG_CHECK(comm_exchange(c->comm, nullptr, 0, nullptr, f, n, c->p.M, c->p.P, c->stream, false));
+    QG_CHECK(comm_exchange(c->comm, nullptr, 0, nullptr, f, n, c->row_words(), c->p.P, c->stream, false));
     c->ghosts_pending = false;
     return QG_OK;
 }
 
-int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
-    if (!c || timestep < 1) return QG_ERR_INVALID_ARG;
-    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
+extern "C++" {
+template <class T>
+static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     const qg_params &p = c->p;
-    QG_HIP(hipSetDevice(c->device));
     const int zh = c->heads[0], ph = c->heads[1], fh = c->heads[2];
     const int zn = (zh + 2) % 3, fn = (fh + 2) % 3;
-    TendArgs a{};
+    TendArgsT<T> a{};
     a.M = p.M;
     a.P = p.P;
     a.ld = p.M + 2;
@@ -248,12 +260,12 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     a.j1 = (int)p.P;
     a.write_ghost_rows = !c->distributed;
     for (int l = 0; l < 2; ++l) {
-        a.zeta[l] = c->field(c->zeta, l, zh);
-        a.psi[l] = c->field(c->psi, l, ph);
-        a.fprev1[l] = c->field(c->fst, l, fh);
-        a.fprev2[l] = c->field(c->fst, l, (fh + 1) % 3);
-        a.zeta_out[l] = c->field(c->zeta, l, zn);
-        a.f_out[l] = c->field(c->fst, l, fn);
+        a.zeta[l] = c->fieldt<T>(c->zeta, l, zh);
+        a.psi[l] = c->fieldt<T>(c->psi, l, ph);
+        a.fprev1[l] = c->fieldt<T>(c->fst, l, fh);
+        a.fprev2[l] = c->fieldt<T>(c->fst, l, (fh + 1) % 3);
+        a.zeta_out[l] = c->fieldt<T>(c->zeta, l, zn);
+        a.f_out[l] = c->fieldt<T>(c->fst, l, fn);
     }
     if (!c->distributed) {
         for (int l = 0; l < 2; ++l) {
@@ -264,18 +276,19 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     } else {
         // halo rows of psi (depth 2; zeta uses the inner two) from the neighbouring slabs,
         // grouped with the pending ghost-row refresh of the previous step's outputs
-        double *f2[4] = {const_cast<double *>(a.psi[0]), const_cast<double *>(a.psi[1]),
-                         const_cast<double *>(a.zeta[0]), const_cast<double *>(a.zeta[1])};
+        double *f2[4] = {c->field(c->psi, 0, ph), c->field(c->psi, 1, ph), c->field(c->zeta, 0, zh),
+                         c->field(c->zeta, 1, zh)};
         // (the f2 fields are the newest psi and zeta: their ghost rows come from the halo rows)
         double *f1[2] = {c->field(c->fst, 0, fh), c->field(c->fst, 1, fh)};
         const int n1 = c->ghosts_pending ? 2 : 0;
-        QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, p.M, p.P, c->stream, c->ghosts_pending));
+        QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, c->row_words(), p.P, c->stream, c->ghosts_pending));
         c->ghosts_pending = false;
-        const int64_t row = p.M + 2;  // halo buffer: [field][4 rows][M+2]; +1 = interior start
+        const int64_t row = p.M + 2;  // halo buffer: [field][4 rows][M+2 elements]; +1 = interior start
+        const T *hb = reinterpret_cast<const T *>(c->halo);
         for (int l = 0; l < 2; ++l)
             for (int h = 0; h < 4; ++h) {
-                a.psi_rows[l].halo[h] = c->halo + ((size_t)(l * 4 + h)) * row + 1;
-                a.zeta_rows[l].halo[h] = c->halo + ((size_t)((2 + l) * 4 + h)) * row + 1;
+                a.psi_rows[l].halo[h] = hb + ((size_t)(l * 4 + h)) * row + 1;
+                a.zeta_rows[l].halo[h] = hb + ((size_t)((2 + l) * 4 + h)) * row + 1;
             }
         QG_CHECK(launch_tendency(a, c->stream));
         c->ghosts_pending = true;
@@ -284,6 +297,14 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     c->heads[2] = fn;
     return QG_OK;
 }
+}  // extern "C++"
+
+int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
+    if (!c || timestep < 1) return QG_ERR_INVALID_ARG;
+    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
+    QG_HIP(hipSetDevice(c->device));
+    return c->esize == sizeof(float) ? evolve_zeta_t<float>(c, timestep) : evolve_zeta_t<double>(c, timestep);
+}
 
 int qg_evolve_psi(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
@@ -291,7 +312,7 @@ int qg_evolve_psi(qg_ctx *c) {
     if (!c->spec && !c->pcg) return QG_ERR_UNSUPPORTED;
     QG_HIP(hipSetDevice(c->device));
     const int zh = c->heads[0], pn = (c->heads[1] + 2) % 3;
-    double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);
+    double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);  // (element type p.dtype)
     const double *z1 = c->field(c->zeta, 0, zh), *z2 = c->field(c->zeta, 1, zh);
     if (c->pcg) {
         const int st = c->pcg->solve(z1, z2, o1, o2, !c->distributed, c->stream,
@@ -324,9 +345,9 @@ int qg_canonicalize(qg_ctx *c) {
     if (!c->zeta) return QG_ERR_NOT_BOUND;
     QG_HIP(hipSetDevice(c->device));
     QG_CHECK(flush_ghosts(c));  // pending ghost-ring refreshes
-    double *bases[3] = {c->zeta, c->psi, c->fst};
-    double *tmp = nullptr;
-    const size_t bytes = sizeof(double) * c->F * 6;
+    void *bases[3] = {c->zeta, c->psi, c->fst};
+    char *tmp = nullptr;
+    const size_t fb = c->esize * c->F, bytes = fb * 6;
     for (int w = 0; w < 3; ++w) {
         if (c->heads[w] == 0) continue;
         if (!tmp) QG_HIP(hipMallocAsync((void **)&tmp, bytes, c->stream));
@@ -334,8 +355,8 @@ int qg_canonicalize(qg_ctx *c) {
         for (int logical = 1; logical <= 3; ++logical) {
             const int phys = (c->heads[w] + logical - 1) % 3;
             for (int l = 0; l < 2; ++l)
-                QG_HIP(hipMemcpyAsync(c->field(bases[w], l, logical - 1), tmp + c->F * (size_t)(l + 2 * phys),
-                                      sizeof(double) * c->F, hipMemcpyDeviceToDevice, c->stream));
+                QG_HIP(hipMemcpyAsync(c->fieldv(bases[w], l, logical - 1), tmp + fb * (size_t)(l + 2 * phys), fb,
+                                      hipMemcpyDeviceToDevice, c->stream));
         }
         c->heads[w] = 0;
     }
@@ -374,29 +395,29 @@ int qg_solver_stats(qg_ctx *c, int *it_poisson, int *it_helm, double *relres_p, 
     return QG_OK;
 }
 
-int qg_snapshot(qg_ctx *c, double *host_zeta, double *host_psi) {
+int qg_snapshot(qg_ctx *c, void *host_zeta, void *host_psi) {
     if (!c || !host_zeta || !host_psi) return QG_ERR_INVALID_ARG;
     if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
     QG_HIP(hipSetDevice(c->device));
     if (!c->snap) {
-        QG_HIP(hipMalloc((void **)&c->snap, sizeof(double) * 4 * c->F));
+        QG_HIP(hipMalloc((void **)&c->snap, c->esize * 4 * c->F));
         QG_HIP(hipStreamCreateWithFlags(&c->snap_stream, hipStreamNonBlocking));
         QG_HIP(hipEventCreateWithFlags(&c->snap_ready, hipEventDisableTiming));
         QG_HIP(hipEventCreateWithFlags(&c->snap_done, hipEventDisableTiming));
     }
     QG_CHECK(flush_ghosts(c));  // multi-GPU: the ghost rows of the newest fields
     if (c->snap_inflight) QG_HIP(hipStreamWaitEvent(c->stream, c->snap_done, 0));  // staging free
-    const size_t fb = sizeof(double) * c->F;
+    const size_t fb = c->esize * c->F;
     for (int l = 0; l < 2; ++l) {
-        QG_HIP(hipMemcpyAsync(c->snap + l * c->F, c->field(c->zeta, l, c->heads[0]), fb, hipMemcpyDeviceToDevice,
+        QG_HIP(hipMemcpyAsync(c->snap + l * fb, c->fieldv(c->zeta, l, c->heads[0]), fb, hipMemcpyDeviceToDevice,
                               c->stream));
-        QG_HIP(hipMemcpyAsync(c->snap + (2 + l) * c->F, c->field(c->psi, l, c->heads[1]), fb,
+        QG_HIP(hipMemcpyAsync(c->snap + (2 + l) * fb, c->fieldv(c->psi, l, c->heads[1]), fb,
                               hipMemcpyDeviceToDevice, c->stream));
     }
     QG_HIP(hipEventRecord(c->snap_ready, c->stream));
     QG_HIP(hipStreamWaitEvent(c->snap_stream, c->snap_ready, 0));
     QG_HIP(hipMemcpyAsync(host_zeta, c->snap, 2 * fb, hipMemcpyDeviceToHost, c->snap_stream));
-    QG_HIP(hipMemcpyAsync(host_psi, c->snap + 2 * c->F, 2 * fb, hipMemcpyDeviceToHost, c->snap_stream));
+    QG_HIP(hipMemcpyAsync(host_psi, c->snap + 2 * fb, 2 * fb, hipMemcpyDeviceToHost, c->snap_stream));
     QG_HIP(hipEventRecord(c->snap_done, c->snap_stream));
     c->snap_inflight = true;
     return QG_OK;

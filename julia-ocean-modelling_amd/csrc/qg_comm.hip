@@ -117,7 +117,9 @@ static int copy_rows(const RowCopies &rc, hipStream_t s) {
 //   f1[0..n1): refresh of the ghost rows (memory rows 0 and P+1) in place
 // Messages: [send -> next, send -> prev], [recv <- prev, recv <- next]; with two ranks
 // (prev == next) the two messages per peer match in this posting order.
-int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t M,
+// ld = row length in 8-byte words ((M+2) for F64 fields, (M+2)/2 for F32 fields: the rows
+// move as raw words, their element type does not matter here)
+int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t ld,
                   int64_t P, hipStream_t s, bool ghost_f2) {
     Comm *c = static_cast<Comm *>(comm);
     if (!c || (!c->nccl && !c->sr)) return QG_ERR_RCCL;
@@ -126,7 +128,6 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
     if (rows == 0) return QG_OK;
     const int G = c->nranks;
     const int next = (c->rank + 1) % G, prev = (c->rank - 1 + G) % G;
-    const int64_t ld = M + 2;
     const size_t need = (size_t)4 * rows * ld;
     if (need > c->stage_n) {
         if (c->stage) (void)hipFree(c->stage);
@@ -183,8 +184,8 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
 // depth == 2: halo rows into halo_buf; depth == -1: ghost-row refresh in place
 int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
               hipStream_t s) {
-    if (depth == 2) return comm_exchange(comm, fields, nfields, halo_buf, nullptr, 0, M, P, s, false);
-    return comm_exchange(comm, nullptr, 0, nullptr, fields, nfields, M, P, s, false);
+    if (depth == 2) return comm_exchange(comm, fields, nfields, halo_buf, nullptr, 0, M + 2, P, s, false);
+    return comm_exchange(comm, nullptr, 0, nullptr, fields, nfields, M + 2, P, s, false);
 }
 
 }  // namespace qg

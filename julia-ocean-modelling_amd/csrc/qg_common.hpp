@@ -46,8 +46,9 @@ __device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -
 // Write v at interior (i, j) and at every ghost cell that is a periodic image of it
 // (edges and the diagonal corners of update_doubly_periodic_bc!).  ghost_rows = 0 skips the
 // images in rows -1 / P (multi-GPU slabs get those rows from their neighbours).
-__device__ __forceinline__ void store_with_ghosts(double *out, int64_t ld, int64_t M, int64_t P,
-                                                  int64_t i, int64_t j, double v, bool ghost_rows) {
+template <class T>
+__device__ __forceinline__ void store_with_ghosts(T *out, int64_t ld, int64_t M, int64_t P,
+                                                  int64_t i, int64_t j, T v, bool ghost_rows) {
     const int64_t mi = i + 1, mj = j + 1;
     out[fidx(mi, mj, ld)] = v;
     const bool lo_i = (i == 0), hi_i = (i == M - 1);
@@ -67,7 +68,8 @@ __device__ __forceinline__ void store_with_ghosts(double *out, int64_t ld, int64
 // Same as store_with_ghosts for a whole row j that the caller walks: `row` = out + (j+1)*ld
 // and the ghost-row target `grow` (row 0 when j == P-1, row P+1 when j == 0, else nullptr)
 // are wave-uniform, so every store is an SGPR base + 32-bit lane offset.
-__device__ __forceinline__ void store_row_with_ghosts(double *row, double *grow, int M, int i, double v) {
+template <class T>
+__device__ __forceinline__ void store_row_with_ghosts(T *row, T *grow, int M, int i, T v) {
     row[i + 1] = v;
     if (i == M - 1) row[0] = v;
     if (i == 0) row[M + 1] = v;
@@ -78,7 +80,8 @@ __device__ __forceinline__ void store_row_with_ghosts(double *row, double *grow,
     }
 }
 
-__device__ __forceinline__ double *ghost_row_target(double *out, int64_t ld, int64_t P, int64_t j, bool ghost_rows) {
+template <class T>
+__device__ __forceinline__ T *ghost_row_target(T *out, int64_t ld, int64_t P, int64_t j, bool ghost_rows) {
     if (!ghost_rows) return nullptr;
     if (j == P - 1) return out;                                     // ghost row j = -1
     if (j == 0) return out + static_cast<size_t>(P + 1) * ld;       // ghost row j = P
@@ -117,13 +120,18 @@ inline Derived derive(const qg_params &m) {
 }
 
 // ---- stencil / tendency launchers (qg_stencil.hip) ----------------------------------
-struct RowSrc {
+// T = element type of the state fields (double: the reference's Float64; float: the F32
+// build of BASELINE config 5)
+template <class T>
+struct RowSrcT {
     // Rows outside [0, P) of a field come from these pointers (interior element 0 of the
     // row, i.e. already offset by the left ghost): index 0,1 = rows -2,-1; 2,3 = rows P, P+1.
-    const double *halo[4];
+    const T *halo[4];
 };
+using RowSrc = RowSrcT<double>;
 
-struct TendArgs {
+template <class T>
+struct TendArgsT {
     int64_t M, P, ld;          // interior sizes; ld = M + 2
     double dx, visc, dt, U, r;
     double beta[2];
@@ -132,24 +140,27 @@ struct TendArgs {
     int j2, j3;                // optional second range [j2, j3) (empty: j3 <= j2)
     int write_ghost_rows;      // single-GPU: refresh ghost rows -1 and P
     // per layer pointers (field base = element (0,0) incl. ghosts)
-    const double *zeta[2];
-    const double *psi[2];
-    const double *fprev1[2];   // F(t-1), F(t-2) for AB3
-    const double *fprev2[2];
-    double *zeta_out[2];
-    double *f_out[2];
-    RowSrc zeta_rows[2];
-    RowSrc psi_rows[2];
+    const T *zeta[2];
+    const T *psi[2];
+    const T *fprev1[2];   // F(t-1), F(t-2) for AB3
+    const T *fprev2[2];
+    T *zeta_out[2];
+    T *f_out[2];
+    RowSrcT<T> zeta_rows[2];
+    RowSrcT<T> psi_rows[2];
 };
+using TendArgs = TendArgsT<double>;
 
-int launch_tendency(const TendArgs &a, hipStream_t s);
+int launch_tendency(const TendArgsT<double> &a, hipStream_t s);
+int launch_tendency(const TendArgsT<float> &a, hipStream_t s);
 int launch_laplace(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
 int launch_cd(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
 int launch_arakawa(const double *z, const double *p, double *out, int64_t M, int64_t P, double dx,
                    hipStream_t s);
 int launch_fill_ghosts(double *b, int64_t M, int64_t P, hipStream_t s);
 int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s);
-int launch_initialise_global(double *zeta, double *psi, double *f_store, int64_t M, int64_t P,
+// esize = sizeof(element) of the state fields (8 or 4)
+int launch_initialise_global(void *zeta, void *psi, void *f_store, int esize, int64_t M, int64_t P,
                              int64_t P_total, int64_t j_offset, double amp, double S1, double S2,
                              double dx, uint64_t seed1, uint64_t seed2, hipStream_t s);
 

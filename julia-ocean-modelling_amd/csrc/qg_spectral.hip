@@ -38,6 +38,23 @@ struct Geo {
     static constexpr int EP = (N + T - 1) / T;  // row elements per thread
 };
 
+// Storage of the fields (S) and of the spectral intermediate u: double2 for F64 states,
+// float2 for F32 states; the transform and the recurrences always run in F64.
+template <class S>
+struct Store;
+template <>
+struct Store<double> {
+    using C = double2;
+    __device__ static C c(double2 v) { return v; }
+};
+template <>
+struct Store<float> {
+    using C = float2;
+    __device__ static C c(double2 v) { return make_float2((float)v.x, (float)v.y); }
+};
+__device__ __forceinline__ double2 d2(double2 v) { return v; }
+__device__ __forceinline__ double2 d2(float2 v) { return make_double2(v.x, v.y); }
+
 __device__ __forceinline__ double2 cfma(double s, double2 x, double2 y) {  // s*x + y
     return make_double2(s * x.x + y.x, s * x.y + y.y);
 }
@@ -45,8 +62,9 @@ __device__ __forceinline__ double2 cfma(double s, double2 x, double2 y) {  // s*
 // ------------------------------------------------------------------------------------
 // pass A: project + row DFT + chunk-local backward filter (one workgroup per chunk)
 // ------------------------------------------------------------------------------------
-template <int N>
+template <int N, class S>
 __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a) {
+    using US = typename Store<S>::C;
     using G = Geo<N>;
     constexpr int T = G::T, KQ = G::KQ, EP = G::EP, NH = N / 2;
     using Plan = FftPlan<N, T>;
@@ -81,8 +99,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     // for LDS traffic, so the global loads stay in flight across the FFT)
     double pf1[EP], pf2[EP];
     auto load_row = [&](int j) {
-        const double *r1 = a.in1 + fidx(1, j + 1, ld);
-        const double *r2 = a.in2 + fidx(1, j + 1, ld);
+        const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
+        const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
 #pragma unroll
         for (int p = 0; p < EP; ++p) {
             const int i = t + p * T;
@@ -114,7 +132,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
             double2 unused[Plan::R_LAST];
             FwdLds::run(b0, b1, twl, unused);
         }
-        double2 *Urow = a.U + (size_t)j * 2 * KS;
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
@@ -131,8 +149,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                         const double2 r0 = a.crr[o0], rN = a.crr[oN];
                         u[q][s] = make_double2(a.ccs[o0] * B[s].x + r0.x * u[q][s].x,
                                                a.ccs[oN] * B[s].y + rN.x * u[q][s].y);
-                        Urow[s * KS] = make_double2(u[q][s].x, 0);
-                        Urow[s * KS + NH] = make_double2(u[q][s].y, 0);
+                        Urow[s * KS] = Store<S>::c(make_double2(u[q][s].x, 0));
+                        Urow[s * KS + NH] = Store<S>::c(make_double2(u[q][s].y, 0));
                         bw[q][s] = make_double2(bw[q][s].x * r0.y + u[q][s].x, bw[q][s].y * rN.y + u[q][s].y);
                     }
                 } else {
@@ -144,7 +162,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                         const int o = s * KS + k;
                         const double2 rr = a.crr[o];
                         u[q][s] = cfma(rr.x, u[q][s], cscale(B[s], a.ccs[o]));
-                        Urow[s * KS + k] = u[q][s];
+                        Urow[s * KS + k] = Store<S>::c(u[q][s]);
                         bw[q][s] = cfma(rr.y, bw[q][s], u[q][s]);
                     }
                 }
@@ -528,8 +546,9 @@ __device__ __forceinline__ void chunk_carry(const SpecArgs &a, int s, int k, int
     w = wi;
 }
 
-template <int N>
+template <int N, class S>
 __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a) {
+    using US = typename Store<S>::C;
     using G = Geo<N>;
     constexpr int T = G::T, KQ = G::KQ, EP = G::EP, NH = N / 2;
     using Plan = FftPlan<N, T>;
@@ -559,14 +578,14 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     // packs the real lines k = 0 (.x) and k = N/2 (.y).
     double2 upf[KQ][2];
     auto load_u = [&](int j) {
-        const double2 *Urow = a.U + (size_t)j * 2 * KS;
+        const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS;
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
             if (NH % T == 0 || k < NH) {
 #pragma unroll
                 for (int s = 0; s < 2; ++s)
-                    upf[q][s] = k == 0 ? make_double2(Urow[s * KS].x, Urow[s * KS + NH].x) : Urow[s * KS + k];
+                    upf[q][s] = k == 0 ? make_double2(Urow[s * KS].x, Urow[s * KS + NH].x) : d2(Urow[s * KS + k]);
             }
         }
     };
@@ -650,10 +669,11 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         __syncthreads();
         double2 xo[Plan::R_LAST];  // last FFT pass output in registers: element t + r*T
         Inv::run(b0, b1, twl, xo);
-        double *row1 = a.out1 + (size_t)(j + 1) * ld;
-        double *grow1 = ghost_row_target(a.out1, ld, Pl, j, a.write_ghost_rows);
-        double *row2 = a.out2 ? a.out2 + (size_t)(j + 1) * ld : nullptr;
-        double *grow2 = a.out2 ? ghost_row_target(a.out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
+        S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
+        S *row1 = out1 + (size_t)(j + 1) * ld;
+        S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
+        S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
+        S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
 #pragma unroll
         for (int p = 0; p < EP; ++p) {
             const int i = t + p * T;
@@ -662,8 +682,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                 if constexpr (Plan::REG_OUT) z = xo[p];
                 else z = Xb[lay<Plan::LAST_NS>(i)];
                 const double x1 = z.x - pin, x2 = z.y;
-                store_row_with_ghosts(row1, grow1, N, i, a.pin_out[0] * x1 + a.pin_out[1] * x2);
-                if (row2) store_row_with_ghosts(row2, grow2, N, i, a.pin_out[2] * x1 + a.pin_out[3] * x2);
+                store_row_with_ghosts(row1, grow1, N, i, (S)(a.pin_out[0] * x1 + a.pin_out[1] * x2));
+                if (row2) store_row_with_ghosts(row2, grow2, N, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
             }
         }
         if constexpr (Inv::b0_read_late) __syncthreads();  // the next row's recurrence writes b0
@@ -673,18 +693,23 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 // ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
-template <int N>
-static int launch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
+template <int N, class S>
+static int launch_pass_t(bool passB, const SpecArgs &a, hipStream_t s) {
     const size_t lds = sizeof(double2) * FftPlan<N, Geo<N>::T>::LDS;
     if (passB) {
-        QG_HIP(hipFuncSetAttribute((const void *)spec_passB<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        spec_passB<N><<<a.Nc, Geo<N>::T, lds, s>>>(a);
+        QG_HIP(hipFuncSetAttribute((const void *)spec_passB<N, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        spec_passB<N, S><<<a.Nc, Geo<N>::T, lds, s>>>(a);
     } else {
-        QG_HIP(hipFuncSetAttribute((const void *)spec_passA<N>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        spec_passA<N><<<a.Nc, Geo<N>::T, lds, s>>>(a);
+        QG_HIP(hipFuncSetAttribute((const void *)spec_passA<N, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        spec_passA<N, S><<<a.Nc, Geo<N>::T, lds, s>>>(a);
     }
     QG_LAUNCH_CHECK();
     return QG_OK;
+}
+
+template <int N>
+static int launch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
+    return a.f32 ? launch_pass_t<N, float>(passB, a, s) : launch_pass_t<N, double>(passB, a, s);
 }
 
 static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
@@ -723,7 +748,7 @@ static size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks, double dx,
                          const double alpha[2], int pinned0, const double pin_in[4], const double pin_out[4],
-                         int chunk_rows) {
+                         int chunk_rows, int f32) {
     if (!supports(M, P)) return QG_ERR_UNSUPPORTED;
     if (!(dx > 0) || nranks < 1 || rank < 0 || rank >= nranks || P_total != P * nranks) return QG_ERR_INVALID_ARG;
     const int L = pick_chunk(P, chunk_rows);
@@ -737,6 +762,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.nranks = nranks;
     a.L = L;
     a.Nc = (int)(P / L);
+    a.f32 = f32;
     a.KH = (int)(M / 2 + 1);
     a.KS = (a.KH + 63) & ~63;
     a.dx = dx;
@@ -804,7 +830,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     double2 *d_tw = (double2 *)take(n_tw);
     Coef *d_coef = (Coef *)take(n_coef);
     double *d_hot = (double *)take(n_hot);
-    a.U = (double2 *)take(n_U);
+    a.U = take(n_U);  // double2 (F64 states) or float2 (F32) per element
     a.ULS = (double2 *)take(n_S);
     a.WLS = (double2 *)take(n_S);
     a.UIN = (double2 *)take(n_S);
@@ -844,7 +870,7 @@ SpectralSolver::~SpectralSolver() {
     if (mem_) (void)hipFree(mem_);
 }
 
-int SpectralSolver::solve(const double *in1, const double *in2, double *out1, double *out2, int write_ghost_rows,
+int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *out2, int write_ghost_rows,
                           hipStream_t s, GatherFn gather, void *user, const double *pin_in, const double *pin_out) {
     if (!mem_) return QG_ERR_NOT_BOUND;
     SpecArgs a = a_;

@@ -40,13 +40,14 @@ struct SpecArgs {
     double pin_in[4];         // projection of the inputs
     double pin_out[4];        // back-projection of the outputs
     int write_ghost_rows;
-    const double *in1, *in2;  // (M+2, P+2) fields
-    double *out1, *out2;
+    int f32;                  // the fields are float (F32 state), else double
+    const void *in1, *in2;    // (M+2, P+2) fields
+    void *out1, *out2;
     const double2 *tw;        // M twiddles
     const Coef *coef;         // [2][KS]
     const double2 *crr;       // [2][KS] (r, 1/r) of coef, unit-stride for the row loops
     const double *ccs;        // [2][KS] cs of coef
-    double2 *U;               // [P][2][KS]
+    void *U;                  // [P][2][KS] complex (double2, or float2 for F32 states)
     double2 *ULS, *WLS;       // [Nc][2][KS]
     double2 *UIN, *WIN;       // [Nc][2][KS]
     double *dcpart;           // [Nc]
@@ -74,12 +75,12 @@ class SpectralSolver {
 public:
     // alpha[s]: construct_spA shift; pinned0: system 0 is the pinned Poisson problem
     int init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks, double dx, const double alpha[2],
-             int pinned0, const double pin_in[4], const double pin_out[4], int chunk_rows);
+             int pinned0, const double pin_in[4], const double pin_out[4], int chunk_rows, int f32 = 0);
     ~SpectralSolver();
     static bool supports(int64_t M, int64_t P);
     // enqueue the whole solve; `gather` (may be null) all-gathers rec -> grec across ranks
     typedef int (*GatherFn)(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
-    int solve(const double *in1, const double *in2, double *out1, double *out2, int write_ghost_rows,
+    int solve(const void *in1, const void *in2, void *out1, void *out2, int write_ghost_rows,
               hipStream_t s, GatherFn gather = nullptr, void *user = nullptr, const double *pin_in = nullptr,
               const double *pin_out = nullptr);  // optional per-call projections
     const SpecArgs &args() const { return a_; }

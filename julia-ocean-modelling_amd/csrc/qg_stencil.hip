@@ -41,13 +41,13 @@ __global__ void cd_kernel(const double *__restrict__ u, double *__restrict__ out
 }
 
 // J at one point from accessors Z(a,b), S(a,b) (arakawa.jl:7-62, same evaluation order)
-template <class ZF, class SF>
-__device__ __forceinline__ double arakawa_point(ZF Z, SF S, double den) {
-    const double jpp = (Z(1, 0) - Z(-1, 0)) * (S(0, 1) - S(0, -1)) - (Z(0, 1) - Z(0, -1)) * (S(1, 0) - S(-1, 0));
-    const double jpt = ((Z(1, 0) * (S(1, 1) - S(1, -1)) - Z(-1, 0) * (S(-1, 1) - S(-1, -1))) -
+template <class V, class ZF, class SF>
+__device__ __forceinline__ V arakawa_point(ZF Z, SF S, V den) {
+    const V jpp = (Z(1, 0) - Z(-1, 0)) * (S(0, 1) - S(0, -1)) - (Z(0, 1) - Z(0, -1)) * (S(1, 0) - S(-1, 0));
+    const V jpt = ((Z(1, 0) * (S(1, 1) - S(1, -1)) - Z(-1, 0) * (S(-1, 1) - S(-1, -1))) -
                         Z(0, 1) * (S(1, 1) - S(-1, 1))) +
                        Z(0, -1) * (S(1, -1) - S(-1, -1));
-    const double jtp = ((Z(1, 1) * (S(0, 1) - S(1, 0)) - Z(-1, -1) * (S(-1, 0) - S(0, -1))) -
+    const V jtp = ((Z(1, 1) * (S(0, 1) - S(1, 0)) - Z(-1, -1) * (S(-1, 0) - S(0, -1))) -
                         Z(-1, 1) * (S(0, 1) - S(-1, 0))) +
                        Z(1, -1) * (S(1, 0) - S(0, -1));
     return ((jpp + jpt) + jtp) / den;
@@ -61,7 +61,7 @@ __global__ void arakawa_kernel(const double *__restrict__ z, const double *__res
     const int64_t ld = M + 2, mi = i + 1, mj = j + 1;
     auto Z = [&](int a, int b) { return z[fidx(mi + a, mj + b, ld)]; };
     auto S = [&](int a, int b) { return p[fidx(mi + a, mj + b, ld)]; };
-    store_with_ghosts(out, ld, M, P, i, j, arakawa_point(Z, S, den), true);
+    store_with_ghosts(out, ld, M, P, i, j, arakawa_point<double>(Z, S, den), true);
 }
 
 // update_doubly_periodic_bc! (boundary_conditions.jl:2-13)
@@ -93,8 +93,8 @@ __global__ void fill_ghosts_kernel(double *b, int64_t M, int64_t P, int rows_too
 // j is computed (software pipeline), so HBM latency hides behind the stencil arithmetic.
 // Per interior point: read zeta, psi, [F(t-1), F(t-2)], write zeta+, F (+ ghost images).
 // ------------------------------------------------------------------------------------
-template <int TX, int PF>
-__global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_block) {
+template <int TX, int PF, class T>
+__global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int rows_per_block) {
     constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
     const int layer = blockIdx.z;
     const int t = threadIdx.x;
@@ -108,24 +108,26 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
     const int jb1 = min(jb0 + rows_per_block, second ? a.j3 : a.j1);
     if (jb0 >= jb1) return;  // uniform over the block
 
-    __shared__ double sp[RP][TX + 4];
-    __shared__ double sz[RZ][TX + 2];
-    __shared__ double sl[RL][TX + 2];
+    __shared__ T sp[RP][TX + 4];
+    __shared__ T sz[RZ][TX + 2];
+    __shared__ T sl[RL][TX + 2];
 
-    const double *psi = a.psi[layer];
-    const double *zeta = a.zeta[layer];
-    const RowSrc &prs = a.psi_rows[layer];
-    const RowSrc &zrs = a.zeta_rows[layer];
-    const double idx = 1.0 / a.dx, idx2 = idx * idx;
-    const double cdc = 0.5 * idx;
-    const double den = 12 * (a.dx * a.dx);
+    const T *psi = a.psi[layer];
+    const T *zeta = a.zeta[layer];
+    const RowSrcT<T> &prs = a.psi_rows[layer];
+    const RowSrcT<T> &zrs = a.zeta_rows[layer];
+    // model constants in the state's precision (the same expressions as the F64 path)
+    const T dx = (T)a.dx, idx = T(1) / dx, idx2 = idx * idx;
+    const T cdc = T(0.5) * idx;
+    const T den = T(12) * (dx * dx);
+    const T visc = (T)a.visc, dtT = (T)a.dt, Ut = (T)a.U, rt = (T)a.r;
     const bool small = M < TX + 4;
 
     auto wx = [&](int x) -> int {  // periodic wrap of an interior column index
         if (small) return ((x % M) + M) % M;
         return x < 0 ? x + M : (x >= M ? x - M : x);
     };
-    auto rowp = [&](const double *base, const RowSrc &rs, int j) -> const double * {
+    auto rowp = [&](const T *base, const RowSrcT<T> &rs, int j) -> const T * {
         if (j >= 0 && j < P) return base + fidx(1, j + 1, ld);
         return rs.halo[j < 0 ? j + 2 : (j - P) + 2];
     };
@@ -139,53 +141,53 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
     const bool ab3 = a.ab3 != 0;
 
     // prefetch pipeline PF rows deep: slot 0 is consumed next
-    double pc[PF], ph[PF], zc[PF], zh[PF], f1[PF], f2[PF];
+    T pc[PF], ph[PF], zc[PF], zh[PF], f1[PF], f2[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) pc[k] = ph[k] = zc[k] = zh[k] = f1[k] = f2[k] = 0;
-    auto fetch_psi = [&](int j, double &c, double &h) {
-        const double *r = rowp(psi, prs, j);
+    auto fetch_psi = [&](int j, T &c, T &h) {
+        const T *r = rowp(psi, prs, j);
         c = r[xo];
         if (ph_q >= 0) h = r[xph];
     };
-    auto fetch_zeta = [&](int j, double &c, double &h) {
-        const double *r = rowp(zeta, zrs, j);
+    auto fetch_zeta = [&](int j, T &c, T &h) {
+        const T *r = rowp(zeta, zrs, j);
         c = r[xo];
         if (zh_q >= 0) h = r[xzh];
     };
-    auto fetch_f = [&](int j, double &g1, double &g2) {
+    auto fetch_f = [&](int j, T &g1, T &g2) {
         if (ab3 && has_out) {
             const size_t o = (size_t)(j + 1) * ld;  // uniform row offset
             g1 = (a.fprev1[layer] + o)[i + 1];
             g2 = (a.fprev2[layer] + o)[i + 1];
         }
     };
-    auto commit_psi = [&](int j, double c, double h) {
-        double *d = sp[(j + 2 * RP) % RP];
+    auto commit_psi = [&](int j, T c, T h) {
+        T *d = sp[(j + 2 * RP) % RP];
         d[t + 2] = c;
         if (ph_q >= 0) d[ph_q] = h;
     };
-    auto commit_zeta = [&](int j, double c, double h) {
-        double *d = sz[(j + 2 * RZ) % RZ];
+    auto commit_zeta = [&](int j, T c, T h) {
+        T *d = sz[(j + 2 * RZ) % RZ];
         d[t + 1] = c;
         if (zh_q >= 0) d[zh_q] = h;
     };
     auto lap_row = [&](int j) {  // lap(psi) at row j, LDS positions 0..TX+1 (x0-1 .. x0+TX)
-        const double *pm = sp[(j - 1 + 2 * RP) % RP], *p0 = sp[(j + 2 * RP) % RP], *pp = sp[(j + 1 + 2 * RP) % RP];
-        double *dst = sl[(j + 2 * RL) % RL];
+        const T *pm = sp[(j - 1 + 2 * RP) % RP], *p0 = sp[(j + 2 * RP) % RP], *pp = sp[(j + 1 + 2 * RP) % RP];
+        T *dst = sl[(j + 2 * RL) % RL];
         for (int q = t; q < TX + 2; q += TX) {
             const int c = q + 1;
-            dst[q] = ((((p0[c - 1] + p0[c + 1]) - 4 * p0[c]) + pm[c]) + pp[c]) * idx2;
+            dst[q] = ((((p0[c - 1] + p0[c + 1]) - T(4) * p0[c]) + pm[c]) + pp[c]) * idx2;
         }
     };
 
     // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 straight into LDS
     for (int j = jb0 - 2; j <= jb0 + 2; ++j) {
-        double c = 0, h = 0;
+        T c = 0, h = 0;
         fetch_psi(j, c, h);
         commit_psi(j, c, h);
     }
     for (int j = jb0 - 1; j <= jb0 + 1; ++j) {
-        double c = 0, h = 0;
+        T c = 0, h = 0;
         fetch_zeta(j, c, h);
         commit_zeta(j, c, h);
     }
@@ -205,14 +207,14 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
     lap_row(jb0);
     lap_row(jb0 + 1);
 
-    const double bl = a.beta[layer];
+    const T bl = (T)a.beta[layer];
     for (int j = jb0; j < jb1; ++j) {
         const bool more = j + 2 <= jb1;  // psi row j+3 / zeta row j+2 / lap row j+2 needed
         if (more) {
             commit_psi(j + 3, pc[0], ph[0]);
             commit_zeta(j + 2, zc[0], zh[0]);
         }
-        const double f1c = f1[0], f2c = f2[0];
+        const T f1c = f1[0], f2c = f2[0];
 #pragma unroll
         for (int k = 0; k + 1 < PF; ++k) {
             pc[k] = pc[k + 1];
@@ -233,31 +235,31 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
         __syncthreads();
         if (more) lap_row(j + 2);
         if (has_out) {
-            const double *Lm = sl[(j - 1 + 2 * RL) % RL], *L0 = sl[(j + 2 * RL) % RL], *Lp = sl[(j + 1 + 2 * RL) % RL];
-            const double *Pm = sp[(j - 1 + 2 * RP) % RP], *P0 = sp[(j + 2 * RP) % RP], *Pp = sp[(j + 1 + 2 * RP) % RP];
-            const double *Zm = sz[(j - 1 + 2 * RZ) % RZ], *Z0 = sz[(j + 2 * RZ) % RZ], *Zp = sz[(j + 1 + 2 * RZ) % RZ];
+            const T *Lm = sl[(j - 1 + 2 * RL) % RL], *L0 = sl[(j + 2 * RL) % RL], *Lp = sl[(j + 1 + 2 * RL) % RL];
+            const T *Pm = sp[(j - 1 + 2 * RP) % RP], *P0 = sp[(j + 2 * RP) % RP], *Pp = sp[(j + 1 + 2 * RP) % RP];
+            const T *Zm = sz[(j - 1 + 2 * RZ) % RZ], *Z0 = sz[(j + 2 * RZ) % RZ], *Zp = sz[(j + 1 + 2 * RZ) % RZ];
             const int cl = t + 1;  // centre in sl / sz (x-halo 1)
             const int cp = t + 2;  // centre in sp (x-halo 2)
-            const double biharm = ((((L0[cl - 1] + L0[cl + 1]) - 4 * L0[cl]) + Lm[cl]) + Lp[cl]) * idx2;
-            const double v_term = a.visc * biharm;
+            const T biharm = ((((L0[cl - 1] + L0[cl + 1]) - T(4) * L0[cl]) + Lm[cl]) + Lp[cl]) * idx2;
+            const T v_term = visc * biharm;
             auto Z = [&](int da, int db) {
-                const double *r = db < 0 ? Zm : (db > 0 ? Zp : Z0);
+                const T *r = db < 0 ? Zm : (db > 0 ? Zp : Z0);
                 return r[cl + da];
             };
             auto S = [&](int da, int db) {
-                const double *r = db < 0 ? Pm : (db > 0 ? Pp : P0);
+                const T *r = db < 0 ? Pm : (db > 0 ? Pp : P0);
                 return r[cp + da];
             };
-            const double J_term = arakawa_point(Z, S, den);
-            const double beta_term = bl * (cdc * (P0[cp + 1] - P0[cp - 1]));
-            double last;
-            if (layer == 0) last = a.U * (cdc * (Z0[cl + 1] - Z0[cl - 1]));  // U * cd(zeta)
-            else last = a.r * L0[cl];                                         // r * lap(psi)
-            const double F = ((v_term - J_term) - beta_term) - last;
-            const double zcen = Z0[cl];
-            const double zn = ab3 ? zcen + a.dt * ((((23.0 / 12.0) * F) - ((16.0 / 12.0) * f1c)) + ((5.0 / 12.0) * f2c))
-                                  : zcen + (a.dt * F);
-            double *zo = a.zeta_out[layer], *fo = a.f_out[layer];
+            const T J_term = arakawa_point<T>(Z, S, den);
+            const T beta_term = bl * (cdc * (P0[cp + 1] - P0[cp - 1]));
+            T last;
+            if (layer == 0) last = Ut * (cdc * (Z0[cl + 1] - Z0[cl - 1]));  // U * cd(zeta)
+            else last = rt * L0[cl];                                         // r * lap(psi)
+            const T F = ((v_term - J_term) - beta_term) - last;
+            const T zcen = Z0[cl];
+            const T zn = ab3 ? zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * f1c)) + ((T)(5.0 / 12.0) * f2c))
+                             : zcen + (dtT * F);
+            T *zo = a.zeta_out[layer], *fo = a.f_out[layer];
             const bool gr = a.write_ghost_rows;
             store_row_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
             store_row_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
@@ -269,7 +271,8 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgs a, int rows_per_b
 // Seeded initialise_model: psi and zeta of slot 0, ghosts included, computed directly at
 // the wrapped GLOBAL index (so slabs need no communication).  model.jl:37-62.
 // ------------------------------------------------------------------------------------
-__global__ void initialise_kernel(double *zeta, double *psi, int64_t M, int64_t P, int64_t P_total,
+template <class T>  // computed in F64 (the reference's values), stored as T
+__global__ void initialise_kernel(T *zeta, T *psi, int64_t M, int64_t P, int64_t P_total,
                                   int64_t j_offset, double amp, double S1, double S2, double idx2,
                                   uint64_t seed1, uint64_t seed2) {
     const int64_t mi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;  // memory index incl ghosts
@@ -289,10 +292,10 @@ __global__ void initialise_kernel(double *zeta, double *psi, int64_t M, int64_t 
     };
     const size_t o = fidx(mi, mj, ld);
     const size_t F = (size_t)(M + 2) * (size_t)(P + 2);
-    psi[o] = p1;
-    psi[F + o] = p2;
-    zeta[o] = lap(seed1) + S1 * (p2 - p1);
-    zeta[F + o] = lap(seed2) + S2 * (p1 - p2);
+    psi[o] = (T)p1;
+    psi[F + o] = (T)p2;
+    zeta[o] = (T)(lap(seed1) + S1 * (p2 - p1));
+    zeta[F + o] = (T)(lap(seed2) + S2 * (p1 - p2));
 }
 
 // ------------------------------------------------------------------------------------
@@ -333,11 +336,11 @@ int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s) {
     return QG_OK;
 }
 
-template <int TX, int PF>
-static int launch_tend_variant(const TendArgs &a, int rows, hipStream_t s) {
+template <int TX, int PF, class T>
+static int launch_tend_variant(const TendArgsT<T> &a, int rows, hipStream_t s) {
     const int nA = (a.j1 - a.j0 + rows - 1) / rows, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + rows - 1) / rows : 0;
     dim3 grid((unsigned)((a.M + TX - 1) / TX), (unsigned)(nA + nB), 2);
-    tendency_kernel<TX, PF><<<grid, TX, 0, s>>>(a, rows);
+    tendency_kernel<TX, PF, T><<<grid, TX, 0, s>>>(a, rows);
     QG_LAUNCH_CHECK();
     return QG_OK;
 }
@@ -352,16 +355,17 @@ static int tend_variant() {
     return v;
 }
 
-int launch_tendency(const TendArgs &a, hipStream_t s) {
+template <class T>
+static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
     if (a.j1 - a.j0 <= 0 && a.j3 - a.j2 <= 0) return QG_OK;
     switch (tend_variant()) {
-        case 1: return launch_tend_variant<256, 1>(a, 32, s);
-        case 2: return launch_tend_variant<128, 1>(a, 64, s);
-        case 3: return launch_tend_variant<256, 1>(a, 128, s);
-        case 4: return launch_tend_variant<256, 2>(a, 64, s);
-        case 5: return launch_tend_variant<512, 1>(a, 64, s);
-        case 6: return launch_tend_variant<128, 2>(a, 64, s);
-        case 7: return launch_tend_variant<256, 3>(a, 64, s);
+        case 1: return launch_tend_variant<256, 1, T>(a, 32, s);
+        case 2: return launch_tend_variant<128, 1, T>(a, 64, s);
+        case 3: return launch_tend_variant<256, 1, T>(a, 128, s);
+        case 4: return launch_tend_variant<256, 2, T>(a, 64, s);
+        case 5: return launch_tend_variant<512, 1, T>(a, 64, s);
+        case 6: return launch_tend_variant<128, 2, T>(a, 64, s);
+        case 7: return launch_tend_variant<256, 3, T>(a, 64, s);
         default: {
             // rows per strip: 64 when the grid is large enough to fill the chip with 2048+
             // workgroups, fewer (down to 4) on small grids, where the serial row march and not
@@ -369,23 +373,30 @@ int launch_tendency(const TendArgs &a, hipStream_t s) {
             const int64_t nx = (a.M + 255) / 256, rows_total = (a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0);
             int rows = 64;
             while (rows > 4 && nx * 2 * ((rows_total + rows - 1) / rows) < 2048) rows >>= 1;
-            return launch_tend_variant<256, 1>(a, rows, s);
+            return launch_tend_variant<256, 1, T>(a, rows, s);
         }
     }
 }
 
+int launch_tendency(const TendArgsT<double> &a, hipStream_t s) { return launch_tendency_t(a, s); }
+int launch_tendency(const TendArgsT<float> &a, hipStream_t s) { return launch_tendency_t(a, s); }
+
 // seeded initialise_model; P = local rows, P_total / j_offset place the slab in the global grid
-int launch_initialise_global(double *zeta, double *psi, double *f_store, int64_t M, int64_t P,
+int launch_initialise_global(void *zeta, void *psi, void *f_store, int esize, int64_t M, int64_t P,
                              int64_t P_total, int64_t j_offset, double amp, double S1, double S2,
                              double dx, uint64_t seed1, uint64_t seed2, hipStream_t s) {
     const size_t F = (size_t)(M + 2) * (size_t)(P + 2);
-    QG_HIP(hipMemsetAsync(zeta, 0, sizeof(double) * F * 6, s));
-    QG_HIP(hipMemsetAsync(psi, 0, sizeof(double) * F * 6, s));
-    QG_HIP(hipMemsetAsync(f_store, 0, sizeof(double) * F * 6, s));
+    QG_HIP(hipMemsetAsync(zeta, 0, esize * F * 6, s));
+    QG_HIP(hipMemsetAsync(psi, 0, esize * F * 6, s));
+    QG_HIP(hipMemsetAsync(f_store, 0, esize * F * 6, s));
     const double i = 1.0 / dx;
     dim3 grid((unsigned)((M + 2 + 255) / 256), (unsigned)(P + 2));
-    initialise_kernel<<<grid, 256, 0, s>>>(zeta, psi, M, P, P_total, j_offset, amp, S1, S2, i * i, seed1,
-                                           seed2);
+    if (esize == 8)
+        initialise_kernel<double><<<grid, 256, 0, s>>>((double *)zeta, (double *)psi, M, P, P_total, j_offset, amp,
+                                                       S1, S2, i * i, seed1, seed2);
+    else
+        initialise_kernel<float><<<grid, 256, 0, s>>>((float *)zeta, (float *)psi, M, P, P_total, j_offset, amp,
+                                                      S1, S2, i * i, seed1, seed2);
     QG_LAUNCH_CHECK();
     return QG_OK;
 }

@@ -35,6 +35,7 @@ struct QGParams
     solver::Int32; precond::Int32
     pcg_rtol::Float64
     pcg_maxit::Int32; chunk_rows::Int32
+    dtype::Int32; reserved0::Int32
 end
 
 struct QGStats
@@ -66,11 +67,12 @@ stream_ptr() = AMDGPU.stream().stream   # hipStream_t of the task-local stream
 
 """Parameters of a reference `BaroclinicModel` (model.jl:12-30) in the C struct."""
 function QGParams(model; P_local::Integer=model.P, solver=SOLVER_SPECTRAL, P_fwd=(1.0, -1.0, 1.0, 1.0),
-                  precond::Integer=1, pcg_rtol=1e-12, pcg_maxit::Integer=500, chunk_rows::Integer=0)
+                  precond::Integer=1, pcg_rtol=1e-12, pcg_maxit::Integer=500, chunk_rows::Integer=0,
+                  dtype::Type=Float64)
     QGParams(model.H_1, model.H_2, model.beta, model.Lx, model.Ly, model.dt, model.T, model.U,
              model.M, P_local, model.dx, model.visc, model.r, model.R_d, model.initial_kick,
              Tuple(Float64.(P_fwd)), Int32(solver), Int32(precond), pcg_rtol, Int32(pcg_maxit),
-             Int32(chunk_rows))
+             Int32(chunk_rows), Int32(dtype === Float32 ? 1 : 0), Int32(0))
 end
 
 """
@@ -80,23 +82,23 @@ Device state `zeta`, `psi`, `f_store` as `(M+2, P+2, 2, 3)` `ROCArray{Float64,4}
 reference's layout) plus the library context that owns the solver scratch.  History slots
 rotate instead of being copied; `canonical!(s)` restores the reference's slot order.
 """
-mutable struct QGState
+mutable struct QGState{T<:Union{Float64,Float32}}
     ctx::Ptr{Cvoid}
-    zeta::ROCArray{Float64,4}
-    psi::ROCArray{Float64,4}
-    f_store::ROCArray{Float64,4}
+    zeta::ROCArray{T,4}
+    psi::ROCArray{T,4}
+    f_store::ROCArray{T,4}
 end
 
-function QGState(model; P_local::Integer=model.P, kw...)
-    params = Ref(QGParams(model; P_local=P_local, kw...))
+function QGState(model; P_local::Integer=model.P, dtype::Type=Float64, kw...)
+    params = Ref(QGParams(model; P_local=P_local, dtype=dtype, kw...))
     shape = (model.M + 2, P_local + 2, 2, 3)
-    zeta, psi, fs = AMDGPU.zeros(Float64, shape), AMDGPU.zeros(Float64, shape), AMDGPU.zeros(Float64, shape)
+    zeta, psi, fs = AMDGPU.zeros(dtype, shape), AMDGPU.zeros(dtype, shape), AMDGPU.zeros(dtype, shape)
     ctx = Ref{Ptr{Cvoid}}(C_NULL)
     @qgcheck qg_create ccall((:qg_create, libqg), Cint, (Ptr{QGParams}, Cint, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
                              params, AMDGPU.device_id(AMDGPU.device()) - 1, stream_ptr(), ctx)
-    @qgcheck qg_bind_state ccall((:qg_bind_state, libqg), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+    @qgcheck qg_bind_state ccall((:qg_bind_state, libqg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
                                  ctx[], pointer(zeta), pointer(psi), pointer(fs))
-    s = QGState(ctx[], zeta, psi, fs)
+    s = QGState{dtype}(ctx[], zeta, psi, fs)
     finalizer(x -> ccall((:qg_destroy, libqg), Cint, (Ptr{Cvoid},), x.ctx), s)
     s
 end
@@ -145,8 +147,8 @@ end
 """`snapshot!(s, zeta_host, psi_host)`: enqueue a copy of the newest `zeta[:,:,:,1]`,
 `psi[:,:,:,1]` into (M+2, P+2, 2) host arrays (page-locked via `AMDGPU.Mem.pin` for an
 asynchronous copy); `snapshot_wait(s)` blocks until they are complete."""
-snapshot!(s::QGState, zh::Array{Float64,3}, ph::Array{Float64,3}) =
-    @qgcheck qg_snapshot ccall((:qg_snapshot, libqg), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}),
+snapshot!(s::QGState{T}, zh::Array{T,3}, ph::Array{T,3}) where {T} =
+    @qgcheck qg_snapshot ccall((:qg_snapshot, libqg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
                                s.ctx, zh, ph)
 snapshot_wait(s::QGState) = @qgcheck qg_snapshot_wait ccall((:qg_snapshot_wait, libqg), Cint, (Ptr{Cvoid},), s.ctx)
 
@@ -159,7 +161,7 @@ function run_model(model, file_name::String, save_results::Bool;
     sample_timestep = 2 * floor(Int, 86400.0 / model.dt)           # run_model.jl:59
     s = initialise_model(model; kw...)
     shape = (model.M + 2, model.P + 2, 2)
-    zh, ph = Array{Float64}(undef, shape), Array{Float64}(undef, shape)
+    zh, ph = similar(Array(s.zeta), shape), similar(Array(s.psi), shape)
     if save_results
         snapshot!(s, zh, ph); snapshot_wait(s)
         write(file_name, "zeta_0", copy(zh)); write(file_name, "psi_0", copy(ph))

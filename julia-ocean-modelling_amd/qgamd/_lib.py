@@ -14,6 +14,7 @@ LIB_PATH = os.environ.get("QGMI355_LIB") or os.path.join(PKG_DIR, "lib", "libqgm
 
 QG_OK = 0
 QG_SOLVER_SPECTRAL = 0
+QG_F64, QG_F32 = 0, 1
 QG_SOLVER_PCG = 1
 QG_PRECOND_NONE = 0
 QG_PRECOND_SPECTRAL = 1
@@ -32,6 +33,7 @@ class QgParams(C.Structure):
         ("solver", C.c_int32), ("precond", C.c_int32),
         ("pcg_rtol", C.c_double),
         ("pcg_maxit", C.c_int32), ("chunk_rows", C.c_int32),
+        ("dtype", C.c_int32), ("reserved0", C.c_int32),
     ]
 
 

@@ -117,7 +117,7 @@ def P_inv_matrix(m):  # model.jl:90-99
 
 
 def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_local=None,
-              precond=_lib.QG_PRECOND_SPECTRAL, pcg_rtol=1e-12, pcg_maxit=500):
+              precond=_lib.QG_PRECOND_SPECTRAL, pcg_rtol=1e-12, pcg_maxit=500, dtype=_lib.QG_F64):
     p = QgParams()
     _lib.lib().qg_default_params(C.byref(p))
     for n in ("H_1", "H_2", "beta", "Lx", "Ly", "dt", "T", "U", "dx", "visc", "r", "R_d",
@@ -133,6 +133,7 @@ def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_loc
     p.pcg_rtol = float(pcg_rtol)
     p.pcg_maxit = int(pcg_maxit)
     p.chunk_rows = int(chunk_rows)
+    p.dtype = int(dtype)
     return p
 
 
@@ -161,11 +162,11 @@ def _check_field(t, M, P):
         raise ValueError(f"field shape {tuple(t.shape)} does not match (P+2, M+2) = {(P + 2, M + 2)}")
 
 
-def device_zeros(m, P_local=None, device="cuda"):
+def device_zeros(m, P_local=None, device="cuda", dtype=None):
     """zeros(M+2, P+2, 2, 3) in Julia layout -> tensor (3, 2, P+2, M+2)."""
     torch = _torch()
     P = m.P if P_local is None else P_local
-    return torch.zeros((3, 2, P + 2, m.M + 2), dtype=torch.float64, device=device)
+    return torch.zeros((3, 2, P + 2, m.M + 2), dtype=torch.float64 if dtype is None else dtype, device=device)
 
 
 class State:
@@ -179,15 +180,21 @@ class State:
 
     def __init__(self, m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0,
                  device=None, rank=0, nranks=1, P_local=None, precond=_lib.QG_PRECOND_SPECTRAL,
-                 pcg_rtol=1e-12, pcg_maxit=500):
+                 pcg_rtol=1e-12, pcg_maxit=500, dtype=None):
+        """dtype: torch.float64 (default, the reference's arithmetic) or torch.float32 (the
+        F32 state of BASELINE config 5; spectral solver only)."""
         torch = _torch()
         self.model = m
         self.P_local = m.P if P_local is None else P_local
         self.device = torch.cuda.current_device() if device is None else device
-        self.zeta = device_zeros(m, self.P_local)
-        self.psi = device_zeros(m, self.P_local)
-        self.f_store = device_zeros(m, self.P_local)
-        self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local, precond, pcg_rtol, pcg_maxit)
+        self.dtype = torch.float64 if dtype is None else dtype
+        if self.dtype not in (torch.float64, torch.float32):
+            raise ValueError("dtype must be torch.float64 or torch.float32")
+        self.zeta = device_zeros(m, self.P_local, dtype=self.dtype)
+        self.psi = device_zeros(m, self.P_local, dtype=self.dtype)
+        self.f_store = device_zeros(m, self.P_local, dtype=self.dtype)
+        self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local, precond, pcg_rtol, pcg_maxit,
+                                _lib.QG_F32 if self.dtype == torch.float32 else _lib.QG_F64)
         self._ctx = C.c_void_p()
         call("qg_create", C.byref(self.params), int(self.device), _stream_ptr(), C.byref(self._ctx))
         call("qg_bind_state", self._ctx, _ptr(self.zeta), _ptr(self.psi), _ptr(self.f_store))

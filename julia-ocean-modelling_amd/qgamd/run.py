@@ -64,7 +64,7 @@ class SnapshotWriter:
         torch = _torch()
         self.st = state
         shape = (2, state.P_local + 2, state.model.M + 2)  # = Julia (M+2, P+2, 2)
-        self.bufs = [tuple(torch.empty(shape, dtype=torch.float64, pin_memory=True) for _ in range(2))
+        self.bufs = [tuple(torch.empty(shape, dtype=state.dtype, pin_memory=True) for _ in range(2))
                      for _ in range(2)]
         self.zf = zipfile.ZipFile(file_name, "w", compression=zipfile.ZIP_STORED, allowZip64=True)
         self.pool = cf.ThreadPoolExecutor(max_workers=1)

@@ -1,0 +1,110 @@
+"""The Float32 state (BASELINE config 5: 8192^2 F32 per GPU).  The reference is Float64 only,
+so the F32 path is checked against the F64 C oracle with an F32 tolerance stated here:
+  zeta: relative RMS < 1e-6 (F32 roundoff, measured ~1e-7);
+  psi:  relative RMS < 5e-3 (the inverse Laplacian amplifies the F32 rounding of zeta in the
+        gravest modes, more the wider the rows; measured 6e-6 at 64^2, 3e-4 at 1024^2,
+        2.3e-3 at 8192 x 16).
+plus: the multi-rank F32 path matches the single-GPU F32 run (1e-5), and F32 refuses PCG."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+    from oracle import qg_oracle, qg_ref
+    qg_oracle.build()
+    return torch, qgamd, qg_oracle, qg_ref
+
+
+@pytest.mark.parametrize("N,P,steps", [(64, 64, 10), (256, 128, 10), (1024, 64, 6), (8192, 16, 3)])
+def test_f32_against_f64_oracle(env, N, P, steps):
+    torch, qg, O, R = env
+    m = qg.bench_model(N, P=P, dt=60.0)
+    st = qg.run_model_no_output(m, nsteps=steps, dtype=torch.float32)
+    assert st.zeta.dtype == torch.float32
+    ref = O.State(R.bench_model(N, P=P, dt=60.0)).run(steps)
+    z = st.to_numpy("zeta")[:, :, :, 0].astype(np.float64)
+    p = st.to_numpy("psi")[:, :, :, 0].astype(np.float64)
+    assert rel(z, ref.zeta[:, :, :, 0]) < 1e-6
+    assert rel(p, ref.psi[:, :, :, 0]) < 5e-3
+
+
+def test_f32_initial_conditions_are_the_rounded_f64_ones(env):
+    torch, qg, O, R = env
+    m = qg.bench_model(64)
+    a = qg.initialise_model(m, dtype=torch.float32).to_numpy("psi")
+    b = qg.initialise_model(m).to_numpy("psi")
+    assert np.array_equal(a, b.astype(np.float32))
+
+
+def test_f32_refuses_pcg(env):
+    torch, qg, O, R = env
+    with pytest.raises(qg.QGError) as e:
+        qg.State(qg.bench_model(32), solver=1, dtype=torch.float32)
+    assert e.value.status == -2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, M, P, steps, outdir):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import qgamd
+    from qgamd.hostcomm import TorchDistTransport
+    st = qgamd.State(qgamd.bench_model(M, P=P), P_local=P // world, dtype=torch.float32)
+    TorchDistTransport().attach(st, world, rank)
+    st.initialise()
+    st.run(1, steps)
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **{n: st.to_numpy(n) for n in ("zeta", "psi", "f_store")})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_f32_slabs_match_single_gpu(env):
+    torch, qg, O, R = env
+    import torch.multiprocessing as mp
+    world, M, P, steps = 2, 64, 64, 5
+    ref = qg.run_model_no_output(qg.bench_model(M, P=P), nsteps=steps, dtype=torch.float32)
+    g = {n: ref.to_numpy(n).astype(np.float64) for n in ("zeta", "psi", "f_store")}
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+        assert all(p.exitcode == 0 for p in procs)
+        Pl = P // world
+        for r in range(world):
+            loc = np.load(os.path.join(d, f"rank{r}.npz"))
+            for n in ("zeta", "psi", "f_store"):
+                want = g[n][:, r * Pl: r * Pl + Pl + 2]
+                assert rel(loc[n].astype(np.float64), want) < 1e-5, (r, n)
