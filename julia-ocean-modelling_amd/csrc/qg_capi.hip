@@ -481,7 +481,6 @@ int qg_comm_init_host(qg_ctx *c, int nranks, int rank, qg_allgather_fn allgather
 int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], const int pinned[2],
                      const double proj_in[4], const double proj_out[4], int kind, int precond, int device,
                      void *stream, qg_solver **out) {
-    (void)precond;
     if (!out || !alpha || !pinned || !proj_in || !proj_out) return QG_ERR_INVALID_ARG;
     *out = nullptr;
     if (kind != QG_SOLVER_SPECTRAL && kind != QG_SOLVER_PCG) return QG_ERR_INVALID_ARG;
