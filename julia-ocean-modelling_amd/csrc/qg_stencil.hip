@@ -10,6 +10,7 @@
 //   eulers_method / AB3   src/model.jl:123-136
 //   ghost ring            src/schemes/boundary_conditions.jl:2-13
 //   initialise_model      src/model.jl:37-62
+#include <algorithm>
 #include <cstdlib>
 
 #include "qg_common.hpp"
@@ -94,7 +95,7 @@ __global__ void fill_ghosts_kernel(double *b, int64_t M, int64_t P, int rows_too
 // Per interior point: read zeta, psi, [F(t-1), F(t-2)], write zeta+, F (+ ghost images).
 // ------------------------------------------------------------------------------------
 template <int TX, int PF, class T>
-__global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int rows_per_block) {
+__global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
     constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
     const int layer = blockIdx.z;
     const int t = threadIdx.x;
@@ -102,10 +103,13 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int rows_p
     const int64_t ld = a.ld;
     const int x0 = blockIdx.x * TX;
     const int i = x0 + t;
-    const int nA = (a.j1 - a.j0 + rows_per_block - 1) / rows_per_block;  // blocks of range 1
-    const bool second = (int)blockIdx.y >= nA;
-    const int jb0 = second ? a.j2 + ((int)blockIdx.y - nA) * rows_per_block : a.j0 + blockIdx.y * rows_per_block;
-    const int jb1 = min(jb0 + rows_per_block, second ? a.j3 : a.j1);
+    // strip rows: range A = [j0, j1) split evenly over nyA workgroups along y, then range B
+    const int y = blockIdx.y;
+    const bool second = y >= nyA;
+    const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
+    const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
+    const int jb0 = r0 + (int)(((int64_t)yy * nr) / ny);
+    const int jb1 = r0 + (int)(((int64_t)(yy + 1) * nr) / ny);
     if (jb0 >= jb1) return;  // uniform over the block
 
     __shared__ T sp[RP][TX + 4];
@@ -340,7 +344,40 @@ template <int TX, int PF, class T>
 static int launch_tend_variant(const TendArgsT<T> &a, int rows, hipStream_t s) {
     const int nA = (a.j1 - a.j0 + rows - 1) / rows, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + rows - 1) / rows : 0;
     dim3 grid((unsigned)((a.M + TX - 1) / TX), (unsigned)(nA + nB), 2);
-    tendency_kernel<TX, PF, T><<<grid, TX, 0, s>>>(a, rows);
+    tendency_kernel<TX, PF, T><<<grid, TX, 0, s>>>(a, nA, nB);
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+// Default geometry: a whole number (QG_TEND_WAVES, default 2) of chip-fulls of strips (CUs x
+// resident workgroups per CU, from the occupancy API) -- a grid that is not a multiple leaves
+// a partly idle last "wave" of workgroups -- with rows split evenly over the strips and at
+// least 4 rows per strip.  (4096^2: 0.380 ms vs 0.385 for fixed 64-row strips; 1024^2: 33 vs
+// 38 us.)
+template <class T>
+static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
+    constexpr int TX = 256, PF = 1;
+    static int slots[2] = {0, 0};  // per element type
+    int &sl = slots[sizeof(T) == 4];
+    if (sl == 0) {
+        int dev = 0, cus = 0, per = 0;
+        QG_HIP(hipGetDevice(&dev));
+        QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_kernel<TX, PF, T>, TX, 0));
+        sl = cus * (per > 0 ? per : 1);
+    }
+    static int waves = -1;
+    if (waves < 0) {
+        const char *e = std::getenv("QG_TEND_WAVES");
+        waves = e ? std::max(1, std::atoi(e)) : 2;
+    }
+    const int nx = (int)((a.M + TX - 1) / TX);
+    const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
+    const int target = std::max(1, waves * sl / (2 * nx));  // row workgroups per column strip
+    auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
+    const int nyA = split(rA), nyB = split(rB);
+    dim3 grid((unsigned)nx, (unsigned)(nyA + nyB), 2);
+    tendency_kernel<TX, PF, T><<<grid, TX, 0, s>>>(a, nyA, nyB);
     QG_LAUNCH_CHECK();
     return QG_OK;
 }
@@ -366,15 +403,13 @@ static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
         case 5: return launch_tend_variant<512, 1, T>(a, 64, s);
         case 6: return launch_tend_variant<128, 2, T>(a, 64, s);
         case 7: return launch_tend_variant<256, 3, T>(a, 64, s);
-        default: {
-            // rows per strip: 64 when the grid is large enough to fill the chip with 2048+
-            // workgroups, fewer (down to 4) on small grids, where the serial row march and not
-            // HBM bandwidth sets the time
+        case 8: {  // r01 geometry: 64-row strips, fewer rows on small grids (>= 2048 workgroups)
             const int64_t nx = (a.M + 255) / 256, rows_total = (a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0);
             int rows = 64;
             while (rows > 4 && nx * 2 * ((rows_total + rows - 1) / rows) < 2048) rows >>= 1;
             return launch_tend_variant<256, 1, T>(a, rows, s);
         }
+        default: return launch_tend_balanced(a, s);
     }
 }
 
