@@ -558,9 +558,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
     const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
     fft_init_twiddles<N, T>(twl, a.tw);
-    __syncthreads();
     const int t = threadIdx.x, c = blockIdx.x;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
+    // the chunk's values of the singular line, staged once (a global load per row would sit
+    // on every row's critical path, in front of the transform's barriers)
+    __shared__ double lline[64];  // L <= 64 (pick_chunk)
+    if (a.pinned0 && t < L) lline[t] = a.line[s0 + t];
+    __syncthreads();
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
     const double delta = a.scal[0];
@@ -645,7 +649,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                         const double wy = rN.x * w[q][s].y + (ulN + cu[q][s].y);
                         w[q][s] = make_double2(wx, wy);
                         cu[q][s] = make_double2(cu[q][s].x * r0.y, cu[q][s].y * rN.y);
-                        x0[s] = (s == 0 && sing) ? (line0 + (double)j * line1) + a.line[j] : wx;
+                        x0[s] = (s == 0 && sing) ? (line0 + (double)j * line1) + lline[j - s0] : wx;
                         xN[s] = wy;
                     }
                     b0[0] = make_double2(x0[0], x0[1]);
@@ -736,7 +740,7 @@ bool SpectralSolver::supports(int64_t M, int64_t P) {
 // Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic), small
 // enough that the P / L workgroups of passes A and B cover the 256 CUs, and dividing P.
 static int pick_chunk(int64_t P, int req) {
-    if (req > 0) return (P % req == 0) ? req : -1;
+    if (req > 0) return (P % req == 0 && req <= 64) ? req : -1;
     int cap = 16;
     while (cap > 1 && P / cap < 256) cap >>= 1;
     for (int L = cap; L >= 1; L >>= 1)
