@@ -149,6 +149,24 @@ int qg_synchronize(qg_ctx *ctx);
 int qg_snapshot(qg_ctx *ctx, void *host_zeta, void *host_psi);  /* elements as params.dtype */
 int qg_snapshot_wait(qg_ctx *ctx);
 
+/* ---- diagnostics for monitoring long runs ---------------------------------------------
+ * Of the newest zeta / psi, reduced over the whole (multi-GPU: global) domain; interior
+ * points only (the ghost ring holds periodic copies).  Synchronous: returns when *out is
+ * filled.  Multi-GPU: every rank must call it (one all-gather of a 16-double record through
+ * the transport) and all ranks receive the same values.  Accumulated in F64 in a fixed
+ * order (reproducible run to run).  Field order = the all-gathered record.               */
+typedef struct qg_diag {
+    double zeta_max[2], zeta_min[2]; /* update_max / update_min (run_model.jl:41-53) of     *
+                                      * zeta[:,:,l,1]                                       */
+    double psi_max[2], psi_min[2];   /* the same for psi[:,:,l,1]                           */
+    double zeta_sum[2];  /* sum zeta_l dx^2: the circulation, conserved by the scheme       */
+    double enstrophy[2]; /* 1/2 sum zeta_l^2 dx^2                                           */
+    double energy[2];    /* 1/2 sum |grad psi_l|^2 dx^2, forward differences                */
+    double interface;    /* 1/2 sum (psi_1 - psi_2)^2 dx^2 (x S1*H_1/H: potential energy)   */
+    double reserved;
+} qg_diag;
+int qg_diagnostics(qg_ctx *ctx, qg_diag *out);
+
 /* ---- multi-GPU (one rank per GPU, slab decomposition in y) ---------------------------
  * Rank r owns global rows [r*P, (r+1)*P) of a global M x (nranks*P) grid; the y direction is
  * periodic over the ring of ranks.  Per step the library exchanges halo rows with the two

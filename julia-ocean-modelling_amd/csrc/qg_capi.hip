@@ -20,6 +20,10 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
 int comm_init(void **comm, int nranks, int rank, const char id[128]);
 int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sendrecv_fn sr, void *user);
 int comm_unique_id(char out[128]);
+int diag_record_len();
+size_t diag_scratch_doubles();
+int launch_diagnostics(const void *z0, const void *z1, const void *p0, const void *p1, int esize, int64_t M,
+                       int64_t P, double dx, double *scratch, double *rec, hipStream_t s);
 }  // namespace qg
 
 using namespace qg;
@@ -53,6 +57,8 @@ struct qg_ctx {
     hipStream_t snap_stream = nullptr;
     hipEvent_t snap_ready = nullptr, snap_done = nullptr;
     bool snap_inflight = false;
+    double *diag = nullptr;  // diagnostics scratch: partial records | record | gathered records
+    size_t diag_cap = 0;
     std::unique_ptr<SpectralSolver> spec;
     std::unique_ptr<PcgSolver> pcg;
     int last_status = QG_OK;  // of the last solve (PCG: QG_ERR_NOT_CONVERGED is kept here)
@@ -166,6 +172,7 @@ int qg_destroy(qg_ctx *c) {
     if (c->snap_stream) (void)hipStreamDestroy(c->snap_stream);
     if (c->comm) comm_destroy(c->comm);
     if (c->halo) (void)hipFree(c->halo);
+    if (c->diag) (void)hipFree(c->diag);
     delete c;
     return QG_OK;
 }
@@ -429,6 +436,58 @@ int qg_snapshot_wait(qg_ctx *c) {
     QG_HIP(hipSetDevice(c->device));
     QG_HIP(hipEventSynchronize(c->snap_done));
     c->snap_inflight = false;
+    return QG_OK;
+}
+
+int qg_diagnostics(qg_ctx *c, qg_diag *out) {
+    if (!c || !out) return QG_ERR_INVALID_ARG;
+    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
+    constexpr int NREC = (int)(sizeof(qg_diag) / sizeof(double));
+    static_assert(NREC == 16, "qg_diag is the 16-double diagnostics record");
+    if (diag_record_len() != NREC) return QG_ERR_UNSUPPORTED;
+    QG_HIP(hipSetDevice(c->device));
+    const size_t scratch = diag_scratch_doubles();
+    // sized for the largest world a context can join (a ctx re-attached to a bigger ring reallocates)
+    const size_t need = scratch + (size_t)NREC * c->nranks;
+    if (c->diag && c->diag_cap < need) {
+        QG_HIP(hipStreamSynchronize(c->stream));
+        QG_HIP(hipFree(c->diag));
+        c->diag = nullptr;
+    }
+    if (!c->diag) {
+        QG_HIP(hipMalloc((void **)&c->diag, sizeof(double) * need));
+        c->diag_cap = need;
+    }
+    QG_CHECK(flush_ghosts(c));  // the forward differences read psi's ghost row P+1
+    const int zh = c->heads[0], ph = c->heads[1];
+    double *rec = c->diag + scratch - NREC, *all = c->diag + scratch;
+    QG_CHECK(launch_diagnostics(c->fieldv(c->zeta, 0, zh), c->fieldv(c->zeta, 1, zh), c->fieldv(c->psi, 0, ph),
+                                c->fieldv(c->psi, 1, ph), (int)c->esize, c->p.M, c->p.P, c->p.dx, c->diag, rec,
+                                c->stream));
+    const double *src = rec;
+    if (c->distributed) {
+        QG_CHECK(comm_allgather(c->comm, rec, all, NREC, c->stream));
+        src = all;
+    }
+    const int n = c->distributed ? c->nranks : 1;
+    std::unique_ptr<double[]> h(new (std::nothrow) double[(size_t)NREC * n]);
+    if (!h) return QG_ERR_ALLOC;
+    QG_HIP(hipMemcpyAsync(h.get(), src, sizeof(double) * NREC * n, hipMemcpyDeviceToHost, c->stream));
+    QG_HIP(hipStreamSynchronize(c->stream));
+    double v[NREC];
+    std::memcpy(v, h.get(), sizeof(v));
+    for (int r = 1; r < n; ++r) {  // rank order: the same sums on every rank
+        const double *q = h.get() + (size_t)NREC * r;
+        for (int l = 0; l < 2; ++l) {
+            v[0 + l] = std::fmax(v[0 + l], q[0 + l]);
+            v[2 + l] = std::fmin(v[2 + l], q[2 + l]);
+            v[4 + l] = std::fmax(v[4 + l], q[4 + l]);
+            v[6 + l] = std::fmin(v[6 + l], q[6 + l]);
+        }
+        for (int k = 8; k < NREC; ++k) v[k] += q[k];
+    }
+    v[NREC - 1] = 0.0;
+    std::memcpy(out, v, sizeof(v));
     return QG_OK;
 }
 

@@ -37,6 +37,12 @@ class QgParams(C.Structure):
     ]
 
 
+class QgDiag(C.Structure):
+    _fields_ = [("zeta_max", C.c_double * 2), ("zeta_min", C.c_double * 2), ("psi_max", C.c_double * 2),
+                ("psi_min", C.c_double * 2), ("zeta_sum", C.c_double * 2), ("enstrophy", C.c_double * 2),
+                ("energy", C.c_double * 2), ("interface", C.c_double), ("reserved", C.c_double)]
+
+
 class QgStats(C.Structure):
     _fields_ = [("iters", C.c_int32 * 2), ("relres", C.c_double * 2), ("delta", C.c_double),
                 ("pin", C.c_double)]
@@ -71,6 +77,7 @@ SIGNATURES = [
     ("qg_synchronize", C.c_int, [_vp]),
     ("qg_snapshot", C.c_int, [_vp, _vp, _vp]),
     ("qg_snapshot_wait", C.c_int, [_vp]),
+    ("qg_diagnostics", C.c_int, [_vp, C.POINTER(QgDiag)]),
     ("qg_comm_unique_id", C.c_int, [C.c_char_p]),
     ("qg_comm_init", C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
     ("qg_comm_init_host", C.c_int, [_vp, C.c_int, C.c_int, AllgatherFn, SendrecvFn, _vp]),

@@ -236,6 +236,15 @@ class State:
         call("qg_get_stats", self._ctx, C.byref(s))
         return {"delta": s.delta, "pin": s.pin, "iters": list(s.iters), "relres": list(s.relres)}
 
+    def diagnostics(self):
+        """qg_diagnostics: max / min of the newest zeta and psi per layer (the update_max /
+        update_min of run_model.jl:41-53), circulation, enstrophy, kinetic energy and the
+        interface term, over the global domain (multi-GPU: every rank calls it)."""
+        d = _lib.QgDiag()
+        call("qg_diagnostics", self._ctx, C.byref(d))
+        return {f: (list(getattr(d, f)) if f != "interface" else d.interface)
+                for f, _ in _lib.QgDiag._fields_ if f != "reserved"}
+
     # -- slot rotation -----------------------------------------------------------------
     def slot(self, which, logical):
         w = {"zeta": 0, "psi": 1, "f_store": 2}[which]

@@ -57,6 +57,18 @@ def log_model_params(m, out=print):
     out(f"Total steps = {total_steps}\n")
 
 
+def update_max(current_max: float, matrix) -> float:
+    """run_model.jl:41-46 (``matrix``: numpy / torch array, or a qg_diagnostics maximum)."""
+    m = float(matrix.max()) if hasattr(matrix, "max") else float(matrix)
+    return m if m > current_max else current_max
+
+
+def update_min(current_min: float, matrix) -> float:
+    """run_model.jl:48-53."""
+    m = float(matrix.min()) if hasattr(matrix, "min") else float(matrix)
+    return m if m < current_min else current_min
+
+
 class SnapshotWriter:
     """Incremental .npz writer fed by qg_snapshot (see module docstring)."""
 
@@ -113,9 +125,10 @@ class SnapshotWriter:
 
 
 def run_model(m, file_name: str, save_results: bool, nsteps=None, seeds=(SEED_LAYER1, SEED_LAYER2),
-              log=print, **kw):
+              log=print, monitor=None, **kw):
     """run_model(model, file_name, save_results) (run_model.jl:55-95) on the GPU.  Returns the
-    State (its newest zeta / psi are the reference's return values)."""
+    State (its newest zeta / psi are the reference's return values).  ``monitor(t, diag)``, if
+    given, receives State.diagnostics() at step 0 and at every sample step."""
     torch = _torch()
     log_model_params(m, log)
     t0 = time.perf_counter()
@@ -130,12 +143,17 @@ def run_model(m, file_name: str, save_results: bool, nsteps=None, seeds=(SEED_LA
         writer = SnapshotWriter(st, file_name)
         writer.metadata(create_metadata(m))
         writer.add("0")
+    if monitor is not None:
+        monitor(0, st.diagnostics())
     log("Running simulation... \n")
     try:
         for t in range(1, total + 1):
             st.step(t)
-            if writer is not None and t % sample_timestep == 0:
-                writer.add(str(t))
+            if t % sample_timestep == 0:
+                if writer is not None:
+                    writer.add(str(t))
+                if monitor is not None:
+                    monitor(t, st.diagnostics())
     finally:
         if writer is not None:
             writer.close()

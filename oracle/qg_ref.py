@@ -448,6 +448,38 @@ def run_model_no_output(m, nsteps=None, seeds=(SEED_LAYER1, SEED_LAYER2), callba
     return zeta, psi, f_store
 
 
+def update_max(current_max, matrix):  # run_model.jl:41-46
+    return np.max(matrix) if np.max(matrix) > current_max else current_max
+
+
+def update_min(current_min, matrix):  # run_model.jl:48-53
+    return np.min(matrix) if np.min(matrix) < current_min else current_min
+
+
+def diagnostics(zeta, psi, dx):
+    """The monitoring record of qg_diagnostics from (M+2, P+2, 2, 3) arrays, slot 1 (newest):
+    update_max / update_min of each layer (run_model.jl:41-53, starting from -Inf / +Inf) and
+    the definitional sums (circulation, enstrophy, forward-difference kinetic energy,
+    interface term) -- not part of the reference, so parity unpinned beyond the max / min."""
+    out = {k: [0.0, 0.0] for k in ("zeta_max", "zeta_min", "psi_max", "psi_min", "zeta_sum",
+                                   "enstrophy", "energy")}
+    for l in range(2):
+        z, p = zeta[:, :, l, 0], psi[:, :, l, 0]
+        out["zeta_max"][l] = update_max(-np.inf, z)
+        out["zeta_min"][l] = update_min(np.inf, z)
+        out["psi_max"][l] = update_max(-np.inf, p)
+        out["psi_min"][l] = update_min(np.inf, p)
+        zi = z[1:-1, 1:-1]
+        out["zeta_sum"][l] = zi.sum() * dx * dx
+        out["enstrophy"][l] = 0.5 * (zi * zi).sum() * dx * dx
+        px = p[2:, 1:-1] - p[1:-1, 1:-1]
+        py = p[1:-1, 2:] - p[1:-1, 1:-1]
+        out["energy"][l] = 0.5 * (px * px + py * py).sum()
+    d = psi[1:-1, 1:-1, 0, 0] - psi[1:-1, 1:-1, 1, 0]
+    out["interface"] = 0.5 * (d * d).sum() * dx * dx
+    return out
+
+
 def bench_model(N, dt=30.0 * MINUTES, T=1.0 * DAY, P=None, Lx=4000.0 * KM, Ly=None):
     """The benchmark parameter set of src/benchmarking/julia_bench_parts.jl:6-18."""
     P = N if P is None else P

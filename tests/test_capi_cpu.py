@@ -127,3 +127,16 @@ def test_invalid_parameters_refused_without_touching_the_gpu(qglib):
     assert qglib.qg_evolve_psi(None) == -1
     assert qglib.qg_step(None, 1) == -1
     assert qglib.qg_destroy(None) == 0
+
+
+def test_checkpoint_format_is_checked(tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "julia-ocean-modelling_amd"))
+    import json
+
+    import numpy as np
+    import qgamd
+    bad = tmp_path / "other.npz"
+    np.savez(bad, meta=np.array(json.dumps({"format": "something-else"})))
+    with pytest.raises(ValueError):
+        qgamd.read_checkpoint(str(bad))

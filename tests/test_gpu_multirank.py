@@ -23,7 +23,11 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, M, P, steps, outdir, solver=0):
+def _flat(d):
+    return np.array([x for k in sorted(d) for x in np.atleast_1d(d[k])])
+
+
+def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
@@ -41,19 +45,31 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0):
     st = qgamd.State(m, P_local=P // world, solver=solver)
     TorchDistTransport().attach(st, world, rank)
     st.initialise()
-    st.run(1, steps)
+    if resume_at:
+        # checkpoint after resume_at steps, rebuild the slab from the file, continue
+        st.run(1, resume_at)
+        path = os.path.join(outdir, f"ck{rank}.npz")
+        qgamd.save_checkpoint(st, path, resume_at)
+        del st
+        st, t = qgamd.load_checkpoint(path)
+        TorchDistTransport().attach(st, world, rank)
+        st.run(t, steps - resume_at)
+    else:
+        st.run(1, steps)
     torch.cuda.synchronize()
-    np.savez(os.path.join(outdir, f"rank{rank}.npz"),
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), diag=_flat(st.diagnostics()),
              **{n: st.to_numpy(n) for n in ("zeta", "psi", "f_store")})
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,M,P,steps,solver", [(2, 64, 64, 6, 0), (4, 32, 64, 5, 0), (2, 128, 96, 4, 0),
-                                                     (2, 64, 64, 6, 1), (4, 32, 64, 4, 1)])
-def test_slabs_match_single_gpu(world, M, P, steps, solver):
+@pytest.mark.parametrize("world,M,P,steps,solver,resume_at",
+                         [(2, 64, 64, 6, 0, 0), (4, 32, 64, 5, 0, 0), (2, 128, 96, 4, 0, 0),
+                          (2, 64, 64, 6, 1, 0), (4, 32, 64, 4, 1, 0), (2, 64, 64, 7, 0, 3)])
+def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at):
     """solver 0 = spectral (record all-gather), 1 = PCG with the spectral preconditioner
-    (its dot products and the z halo also cross the slabs)."""
+    (its dot products and the z halo also cross the slabs).  resume_at > 0: every rank
+    checkpoints its slab after that many steps and continues from the file."""
     import torch
     import torch.multiprocessing as mp
 
@@ -64,18 +80,25 @@ def test_slabs_match_single_gpu(world, M, P, steps, solver):
     ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps, solver=solver)
     torch.cuda.synchronize()
     g = {n: ref.to_numpy(n) for n in ("zeta", "psi", "f_store")}
+    gd = _flat(ref.diagnostics())
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, resume_at))
+                 for r in range(world)]
         for p in procs:
             p.start()
         for p in procs:
             p.join(timeout=300)
         assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
         Pl = P // world
+        diags = []
         for r in range(world):
             loc = np.load(os.path.join(d, f"rank{r}.npz"))
+            diags.append(loc["diag"])
+            # qg_diagnostics over the slabs (one record all-gather) = the single-GPU values
+            np.testing.assert_allclose(loc["diag"], gd, rtol=1e-10, atol=1e-10 * np.abs(gd).max())
+            assert np.array_equal(loc["diag"], diags[0])  # every rank gets the same record
             for n in ("zeta", "psi", "f_store"):
                 want = g[n][:, r * Pl: r * Pl + Pl + 2]
                 err = np.linalg.norm(loc[n] - want) / np.linalg.norm(want)

@@ -207,3 +207,20 @@ def test_full_size_invariants_4096(torch, qg):
     p1, p2 = st.current("psi", 1), st.current("psi", 2)
     pt1 = 0.5 * (float(p1[1, 1]) + float(p2[1, 1]))
     assert abs(pt1) < 1e-12 * float(p1.abs().max())
+
+
+@pytest.mark.parametrize("solver", [0, 1])
+def test_physical_projection_option(torch, qg, O, R, solver):
+    """the physically consistent back-projection P_matrix(H_1, H_2) (so that
+    P P^-1 = I, test.jl:195-217) behind qg_params.P_fwd, instead of the reference's
+    P_matrix(H_1, H_1) (model.jl:173).  Same tolerance as the default path, against the C
+    oracle run with the same matrix; it must also differ from the default trajectory."""
+    m = qg.bench_model(64)
+    Pf = R.P_matrix(m.H_1, m.H_2)
+    assert np.allclose(Pf @ R.P_inv_matrix(R.bench_model(64)), np.eye(2))
+    st = qg.run_model_no_output(m, nsteps=30, P_fwd=Pf, solver=solver)
+    ref = O.State(R.bench_model(64), P_fwd=Pf).run(30)
+    assert rel(st.to_numpy("psi"), ref.psi) < TOL
+    assert rel(st.to_numpy("zeta"), ref.zeta) < TOL
+    default = qg.run_model_no_output(m, nsteps=30, solver=solver)
+    assert rel(default.to_numpy("psi"), ref.psi) > 1e-3

@@ -54,6 +54,46 @@ def test_run_matches_scipy_oracle(N, steps):
         assert err < 1e-12, err
 
 
+def test_run_with_physical_projection_matches_scipy_oracle():
+    """The P_fwd = P_matrix(H_1, H_2) option in the C oracle against the
+    literal restatement's evolve_psi(..., P_fwd=...)."""
+    m = R.bench_model(32)
+    Pf = R.P_matrix(m.H_1, m.H_2)
+    zeta, psi = R.initialise_model(m)
+    pc = R.get_poisson_cholesky(m.M, m.P, m.dx)
+    hc = R.get_helmholtz_cholesky(m.M, m.P, m.dx, R.S_eig(m))
+    f = np.zeros((m.M + 2, m.P + 2, 2, 3))
+    for t in range(1, 11):
+        R.evolve_zeta(m, zeta, psi, t, f)
+        R.evolve_psi(m, zeta, psi, pc, hc, P_fwd=Pf)
+    st = O.State(m, P_fwd=Pf).run(10)
+    assert np.linalg.norm(st.psi - psi) / np.linalg.norm(psi) < 1e-12
+
+
+def test_diagnostics_definitions():
+    """oracle diagnostics (qg_diagnostics' checker) on fields with known values."""
+    M = P = 16
+    dx = 2.0
+    z = np.zeros((M + 2, P + 2, 2, 3))
+    p = np.zeros_like(z)
+    x = np.arange(M) * 2 * np.pi / M
+    p[1:-1, 1:-1, 0, 0] = np.sin(x)[:, None]            # psi_1 = sin(2 pi i / M)
+    p[:, :, 0, 0] = R.update_doubly_periodic_bc(p[:, :, 0, 0])
+    z[1:-1, 1:-1, 1, 0] = 3.0
+    z[:, :, 1, 0] = R.update_doubly_periodic_bc(z[:, :, 1, 0])
+    d = R.diagnostics(z, p, dx)
+    assert d["zeta_max"] == [0.0, 3.0] and d["zeta_min"] == [0.0, 3.0]
+    assert d["zeta_sum"][1] == 3.0 * M * P * dx * dx
+    assert d["enstrophy"][1] == 0.5 * 9.0 * M * P * dx * dx
+    # sum_i (sin(x+h) - sin x)^2 = 2 M sin^2(h/2) ... per row, P rows
+    h = 2 * np.pi / M
+    assert np.isclose(d["energy"][0], 0.5 * P * M * 4 * np.sin(h / 2) ** 2 / 2, rtol=1e-13)
+    assert d["energy"][1] == 0.0
+    assert np.isclose(d["interface"], 0.5 * P * (M / 2) * dx * dx, rtol=1e-13)
+    assert R.update_max(5.0, p[:, :, 0, 0]) == 5.0 and R.update_max(0.5, p[:, :, 0, 0]) == 1.0
+    assert R.update_min(5.0, p[:, :, 0, 0]) == -1.0 and R.update_min(-2.0, p[:, :, 0, 0]) == -2.0
+
+
 def test_initial_conditions_bitwise():
     m = R.bench_model(24, P=16)
     z, p = R.initialise_model(m)
