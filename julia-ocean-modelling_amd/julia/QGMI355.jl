@@ -45,6 +45,14 @@ struct QGStats
     pin::Float64
 end
 
+# qg_diag: the 16-double diagnostics record
+struct QGDiag
+    zeta_max::NTuple{2,Float64}; zeta_min::NTuple{2,Float64}
+    psi_max::NTuple{2,Float64}; psi_min::NTuple{2,Float64}
+    zeta_sum::NTuple{2,Float64}; enstrophy::NTuple{2,Float64}; energy::NTuple{2,Float64}
+    interface::Float64; reserved::Float64
+end
+
 const SOLVER_SPECTRAL = Int32(0)
 const SOLVER_PCG = Int32(1)
 
@@ -142,6 +150,31 @@ function stats(s::QGState)
     @qgcheck qg_get_stats ccall((:qg_get_stats, libqg), Cint, (Ptr{Cvoid}, Ptr{QGStats}), s.ctx, r)
     r[]
 end
+
+"""`diagnostics(s)`: max / min of the newest zeta and psi per layer, circulation, enstrophy,
+kinetic energy, interface term over the global domain (every rank calls it)."""
+function diagnostics(s::QGState)
+    r = Ref{QGDiag}()
+    @qgcheck qg_diagnostics ccall((:qg_diagnostics, libqg), Cint, (Ptr{Cvoid}, Ptr{QGDiag}), s.ctx, r)
+    r[]
+end
+
+# run_model.jl:41-53, fed from `diagnostics(s)` instead of a host copy of the fields
+update_max(current_max::Float64, x::Float64) = x > current_max ? x : current_max
+update_min(current_min::Float64, x::Float64) = x < current_min ? x : current_min
+
+"""`save_checkpoint(s, t; write)` / resume: canonicalise, then the caller-owned arrays ARE the
+checkpoint -- store `Array(s.zeta)`, `Array(s.psi)`, `Array(s.f_store)` and `t`; to resume,
+copy them into a fresh `QGState`'s arrays, call `set_slots!(s, (0, 0, 0))` and continue the
+loop at `t + 1` (AB3 reads f_store slots 1-2, so it must be saved with zeta and psi)."""
+function save_checkpoint(s::QGState, t::Integer; write)
+    canonical!(s)
+    AMDGPU.synchronize()
+    write("zeta", Array(s.zeta)); write("psi", Array(s.psi)); write("f_store", Array(s.f_store))
+    write("timestep", Int(t))
+end
+set_slots!(s::QGState, heads::NTuple{3,Integer}) =
+    @qgcheck qg_set_slots ccall((:qg_set_slots, libqg), Cint, (Ptr{Cvoid}, Ptr{Cint}), s.ctx, Cint[heads...])
 
 # --- snapshot output: run_model (run_model.jl:55-95) ---------------------------------------
 """`snapshot!(s, zeta_host, psi_host)`: enqueue a copy of the newest `zeta[:,:,:,1]`,
