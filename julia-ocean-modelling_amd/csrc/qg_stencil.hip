@@ -11,6 +11,7 @@
 //   ghost ring            src/schemes/boundary_conditions.jl:2-13
 //   initialise_model      src/model.jl:37-62
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "qg_common.hpp"
@@ -366,13 +367,18 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
         QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_kernel<TX, PF, T>, TX, 0));
         sl = cus * (per > 0 ? per : 1);
     }
-    static int waves = -1;
-    if (waves < 0) {
+    static int env_waves = -1;
+    if (env_waves < 0) {
         const char *e = std::getenv("QG_TEND_WAVES");
-        waves = e ? std::max(1, std::atoi(e)) : 2;
+        env_waves = e ? std::max(1, std::atoi(e)) : 0;
     }
     const int nx = (int)((a.M + TX - 1) / TX);
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
+    // one chip-full of longer strips from ~1750^2 to ~3500^2 points: the ring prologue (6 rows
+    // read before the first output row) then costs less than the idle tail of a second wave
+    // (tile sweep, profiles/r01/tile_sweep_*.json: 2048^2 106 vs 111 us)
+    const double pts = (double)a.M * (rA + rB);
+    const int waves = env_waves ? env_waves : (pts >= 3.0e6 && pts < 12.0e6 ? 1 : 2);
     const int target = std::max(1, waves * sl / (2 * nx));  // row workgroups per column strip
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -392,9 +398,39 @@ static int tend_variant() {
     return v;
 }
 
+// Explicit tile (tuning knob / the LDS tile sweep of BASELINE config 3): QG_TEND_TILE="WxR"
+// = strips W points wide (one thread per point, W in {64, 128, 256, 512}) and about R rows per
+// workgroup.  0 = unset.
+static void tend_tile(int &w, int &r) {
+    static int tw = -1, tr = 0;
+    if (tw < 0) {
+        tw = 0;
+        const char *e = std::getenv("QG_TEND_TILE");
+        if (e && std::sscanf(e, "%dx%d", &tw, &tr) != 2) tw = 0;
+        if (tw != 64 && tw != 128 && tw != 256 && tw != 512) tw = 0;
+        if (tr < 1) tw = 0;
+    }
+    w = tw;
+    r = tr;
+}
+
 template <class T>
 static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
     if (a.j1 - a.j0 <= 0 && a.j3 - a.j2 <= 0) return QG_OK;
+    int tw, tr;
+    tend_tile(tw, tr);
+    switch (tw) {
+        case 64: return launch_tend_variant<64, 1, T>(a, tr, s);
+        case 128: return launch_tend_variant<128, 1, T>(a, tr, s);
+        case 256: return launch_tend_variant<256, 1, T>(a, tr, s);
+        case 512: return launch_tend_variant<512, 1, T>(a, tr, s);
+        default: break;
+    }
+    if (tend_variant() == 0 && tw == 0) {
+        // ~870^2 .. ~1750^2 points: 128-wide strips of 8 rows (tile sweep: 1024^2 35 vs 38 us)
+        const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
+        if (pts >= 0.75e6 && pts < 3.0e6) return launch_tend_variant<128, 1, T>(a, 8, s);
+    }
     switch (tend_variant()) {
         case 1: return launch_tend_variant<256, 1, T>(a, 32, s);
         case 2: return launch_tend_variant<128, 1, T>(a, 64, s);

@@ -20,5 +20,8 @@ torch.cuda.synchronize()
 tz = sorted(e[0].elapsed_time(e[1]) for e in ev)
 tp = sorted(e[1].elapsed_time(e[2]) for e in ev)
 gb = 96 * n * n / 1e9
-print(json.dumps({"variant": os.environ.get("QG_TEND_VARIANT", "0"), "tend_ms_med": tz[K // 2], "tend_ms_min": tz[0],
+import hashlib
+zsha = hashlib.sha1(st.to_numpy("zeta").tobytes()).hexdigest()
+print(json.dumps({"zeta_sha1": zsha, "tile": os.environ.get("QG_TEND_TILE", ""),
+                  "variant": os.environ.get("QG_TEND_VARIANT", "0"), "tend_ms_med": tz[K // 2], "tend_ms_min": tz[0],
                   "tend_TBs": gb / tz[K // 2], "solve_ms_med": tp[K // 2]}))
