@@ -2,6 +2,7 @@
 // stateless operators.  Everything is enqueued on the caller's stream; nothing in a step
 // allocates, synchronises or touches the host.
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -57,6 +58,17 @@ struct qg_ctx {
     hipStream_t snap_stream = nullptr;
     hipEvent_t snap_ready = nullptr, snap_done = nullptr;
     bool snap_inflight = false;
+    // qg_run: three AB3 steps captured as one HIP graph per slot-rotation state (the heads
+    // return to their values after three steps), replayed on a private stream
+    struct StepGraph {
+        hipGraphExec_t exec = nullptr;
+        int heads[3] = {0, 0, 0};
+    };
+    StepGraph graphs[3];
+    int ngraphs = 0;
+    bool graph_ok = true;  // cleared if capture fails (then qg_run launches step by step)
+    hipStream_t gstream = nullptr;
+    hipEvent_t gev_in = nullptr, gev_out = nullptr;
     double *diag = nullptr;  // diagnostics scratch: partial records | record | gathered records
     size_t diag_cap = 0;
     std::unique_ptr<SpectralSolver> spec;
@@ -115,10 +127,17 @@ static int check_params(const qg_params *p) {
     return QG_OK;
 }
 
+static void drop_graphs(qg_ctx *c) {
+    for (int g = 0; g < c->ngraphs; ++g)
+        if (c->graphs[g].exec) (void)hipGraphExecDestroy(c->graphs[g].exec);
+    c->ngraphs = 0;
+}
+
 static int build_solver(qg_ctx *c) {
     const qg_params &p = c->p;
     const double alpha[2] = {0.0, c->d.Seig};
     QG_HIP(hipSetDevice(c->device));
+    drop_graphs(c);
     c->spec.reset();
     c->pcg.reset();
     if (p.solver == QG_SOLVER_PCG) {
@@ -173,12 +192,17 @@ int qg_destroy(qg_ctx *c) {
     if (c->comm) comm_destroy(c->comm);
     if (c->halo) (void)hipFree(c->halo);
     if (c->diag) (void)hipFree(c->diag);
+    drop_graphs(c);
+    if (c->gstream) (void)hipStreamDestroy(c->gstream);
+    if (c->gev_in) (void)hipEventDestroy(c->gev_in);
+    if (c->gev_out) (void)hipEventDestroy(c->gev_out);
     delete c;
     return QG_OK;
 }
 
 int qg_bind_state(qg_ctx *c, void *zeta, void *psi, void *f_store) {
     if (!c || !zeta || !psi || !f_store) return QG_ERR_INVALID_ARG;
+    drop_graphs(c);
     c->zeta = zeta;
     c->psi = psi;
     c->fst = f_store;
@@ -341,9 +365,74 @@ int qg_step(qg_ctx *c, int64_t timestep) {
     return qg_evolve_psi(c);
 }
 
+// Graph replay of AB3 steps (single GPU, spectral solver: no host round trips in a step),
+// opt-in with QG_GRAPH=1: on ROCm 7.2 / MI355X replaying the captured graph measured slower
+// than launching the same kernels on the stream (0.87x at 128^2 .. 0.99x at 4096^2,
+// tools/graph_bench.py), so stream launches are the default.
+static bool graphs_enabled(const qg_ctx *c) {
+    const char *e = std::getenv("QG_GRAPH");
+    return e && std::atoi(e) != 0 && c->graph_ok && !c->distributed && c->spec && !c->pcg;
+}
+
+// the graph of three AB3 steps starting from the current slot rotation (captured on first use)
+static int step_graph(qg_ctx *c, hipGraphExec_t *out) {
+    for (int g = 0; g < c->ngraphs; ++g)
+        if (std::memcmp(c->graphs[g].heads, c->heads, sizeof(c->heads)) == 0) {
+            *out = c->graphs[g].exec;
+            return QG_OK;
+        }
+    if (c->ngraphs == 3) drop_graphs(c);
+    if (!c->gstream) {
+        QG_HIP(hipStreamCreateWithFlags(&c->gstream, hipStreamNonBlocking));
+        QG_HIP(hipEventCreateWithFlags(&c->gev_in, hipEventDisableTiming));
+        QG_HIP(hipEventCreateWithFlags(&c->gev_out, hipEventDisableTiming));
+    }
+    int heads0[3];
+    std::memcpy(heads0, c->heads, sizeof(heads0));
+    hipStream_t saved = c->stream;
+    c->stream = c->gstream;
+    hipGraph_t graph = nullptr;
+    int st = hipStreamBeginCapture(c->gstream, hipStreamCaptureModeThreadLocal) == hipSuccess ? QG_OK : QG_ERR_HIP;
+    if (st == QG_OK) {
+        for (int k = 0; k < 3 && st == QG_OK; ++k) st = qg_step(c, 3 + k);  // any t >= 3: AB3
+        if (hipStreamEndCapture(c->gstream, &graph) != hipSuccess) st = QG_ERR_HIP;
+    }
+    c->stream = saved;
+    std::memcpy(c->heads, heads0, sizeof(heads0));  // (three steps: the rotation is back anyway)
+    hipGraphExec_t exec = nullptr;
+    if (st == QG_OK && hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) st = QG_ERR_HIP;
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipGetLastError();
+    if (st != QG_OK) {
+        c->graph_ok = false;  // launch step by step from now on
+        return st;
+    }
+    c->graphs[c->ngraphs].exec = exec;
+    std::memcpy(c->graphs[c->ngraphs].heads, heads0, sizeof(heads0));
+    ++c->ngraphs;
+    *out = exec;
+    return QG_OK;
+}
+
 int qg_run(qg_ctx *c, int64_t first_step, int64_t nsteps) {
     if (!c || first_step < 1 || nsteps < 0) return QG_ERR_INVALID_ARG;
-    for (int64_t t = first_step; t < first_step + nsteps; ++t) QG_CHECK(qg_step(c, t));
+    int64_t t = first_step;
+    const int64_t end = first_step + nsteps;
+    for (; t < end && t < 3; ++t) QG_CHECK(qg_step(c, t));  // the Euler steps
+    if (end - t >= 6 && graphs_enabled(c) && c->initialised && c->zeta) {
+        QG_HIP(hipSetDevice(c->device));
+        hipGraphExec_t g = nullptr;
+        if (step_graph(c, &g) == QG_OK) {
+            const int64_t cycles = (end - t) / 3;
+            QG_HIP(hipEventRecord(c->gev_in, c->stream));  // after the caller's earlier work
+            QG_HIP(hipStreamWaitEvent(c->gstream, c->gev_in, 0));
+            for (int64_t k = 0; k < cycles; ++k) QG_HIP(hipGraphLaunch(g, c->gstream));
+            QG_HIP(hipEventRecord(c->gev_out, c->gstream));
+            QG_HIP(hipStreamWaitEvent(c->stream, c->gev_out, 0));  // before the caller's later work
+            t += 3 * cycles;
+        }
+    }
+    for (; t < end; ++t) QG_CHECK(qg_step(c, t));
     return QG_OK;
 }
 

@@ -8,7 +8,8 @@ import qgamd
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 K = 20
-st = qgamd.State(qgamd.bench_model(n, dt=60.0)).initialise()
+dtype = torch.float32 if os.environ.get("QG_TUNE_DTYPE") == "f32" else torch.float64
+st = qgamd.State(qgamd.bench_model(n, dt=60.0), dtype=dtype).initialise()
 for t in range(1, 6):
     st.step(t)
 torch.cuda.synchronize()
@@ -19,7 +20,7 @@ for k in range(K):
 torch.cuda.synchronize()
 tz = sorted(e[0].elapsed_time(e[1]) for e in ev)
 tp = sorted(e[1].elapsed_time(e[2]) for e in ev)
-gb = 96 * n * n / 1e9
+gb = (96 if dtype == torch.float64 else 48) * n * n / 1e9
 import hashlib
 zsha = hashlib.sha1(st.to_numpy("zeta").tobytes()).hexdigest()
 print(json.dumps({"zeta_sha1": zsha, "tile": os.environ.get("QG_TEND_TILE", ""),
