@@ -695,6 +695,230 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 }
 
 // ------------------------------------------------------------------------------------
+// Generic rows (M even, not a power of two, M <= GEN_MMAX): the same passes with the row
+// transform done as a direct DFT in LDS (O(M^2) per row instead of the FFT) -- for the
+// reference's own grid sweeps (julia_bench_parts.jl:19, M = 8:8:128) and any other even M.
+// Everything else (recurrences, chunk summaries, carries, pin, multi-rank closure) is the
+// power-of-two code's, with the row length at run time.
+// ------------------------------------------------------------------------------------
+constexpr int GEN_T = 256;
+constexpr int GEN_MMAX = 2048;
+constexpr int GEN_KQ = GEN_MMAX / 2 / GEN_T;  // wavenumber slots per thread
+
+// X_k = sum_x src[x] W^(k x), W = tw[1] (forward) or its conjugate (inverse)
+template <bool INV>
+__device__ __forceinline__ double2 dft_at(const double2 *src, const double2 *twl, int M, int k) {
+    double2 acc = make_double2(0, 0);
+    int m = 0;  // k x mod M
+    for (int x = 0; x < M; ++x) {
+        double2 w = twl[m];
+        if (INV) w.y = -w.y;
+        acc = cadd(acc, cmul(src[x], w));
+        m += k;
+        if (m >= M) m -= M;
+    }
+    return acc;
+}
+
+template <class S>
+__global__ __launch_bounds__(GEN_T) void spec_passA_gen(SpecArgs a) {
+    using US = typename Store<S>::C;
+    constexpr int T = GEN_T, KQ = GEN_KQ;
+    const int M = (int)a.M, NH = M / 2;
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *b1 = lds + M, *twl = lds + 2 * M;
+    const int t = threadIdx.x, c = blockIdx.x;
+    for (int m = t; m < M; m += T) twl[m] = a.tw[m];
+    const int s0 = c * a.L, e = s0 + a.L - 1;
+    const int KS = a.KS;
+    const int64_t ld = a.ld;
+    double2 u[KQ][2], bw[KQ][2];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            u[q][s] = make_double2(0, 0);
+            bw[q][s] = make_double2(0, 0);
+        }
+    const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
+    double dc = 0;
+    for (int j = e; j >= s0; --j) {
+        const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
+        const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
+        for (int i = t; i < M; i += T) {
+            const double z1 = r1[i], z2 = r2[i];
+            b0[i] = make_double2(p0 * z1 + p1 * z2, p2 * z1 + p3 * z2);
+        }
+        __syncthreads();
+        for (int k = t; k < M; k += T) b1[k] = dft_at<false>(b0, twl, M, k);
+        __syncthreads();
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+            const int k = t + q * T;
+            if (k < NH) {
+                const double2 Zk = b1[k];
+                if (k == 0) {  // the two real lines k = 0 and k = M/2
+                    const double2 Zn = b1[NH];
+                    dc += Zk.x;
+                    a.hline[j] = Zk.x;
+                    const double2 B[2] = {make_double2(Zk.x, Zn.x), make_double2(Zk.y, Zn.y)};
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int o0 = s * KS, oN = s * KS + NH;
+                        const double2 r0 = a.crr[o0], rN = a.crr[oN];
+                        u[q][s] = make_double2(a.ccs[o0] * B[s].x + r0.x * u[q][s].x,
+                                               a.ccs[oN] * B[s].y + rN.x * u[q][s].y);
+                        Urow[s * KS] = Store<S>::c(make_double2(u[q][s].x, 0));
+                        Urow[s * KS + NH] = Store<S>::c(make_double2(u[q][s].y, 0));
+                        bw[q][s] = make_double2(bw[q][s].x * r0.y + u[q][s].x, bw[q][s].y * rN.y + u[q][s].y);
+                    }
+                } else {
+                    const double2 Zm = b1[M - k];
+                    const double2 B[2] = {make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5),
+                                          make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5)};
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int o = s * KS + k;
+                        const double2 rr = a.crr[o];
+                        u[q][s] = cfma(rr.x, u[q][s], cscale(B[s], a.ccs[o]));
+                        Urow[s * KS + k] = Store<S>::c(u[q][s]);
+                        bw[q][s] = cfma(rr.y, bw[q][s], u[q][s]);
+                    }
+                }
+            }
+        }
+        __syncthreads();  // the next row overwrites b0 / b1
+    }
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+        const int k = t + q * T;
+        if (k < NH) {
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const size_t o = ((size_t)c * 2 + s) * KS;
+                if (k == 0) {
+                    const double q0 = a.coef[s * KS].qm1, qN = a.coef[s * KS + NH].qm1;
+                    a.ULS[o] = make_double2(u[q][s].x, 0);
+                    a.ULS[o + NH] = make_double2(u[q][s].y, 0);
+                    a.WLS[o] = make_double2(bw[q][s].x * q0, 0);
+                    a.WLS[o + NH] = make_double2(bw[q][s].y * qN, 0);
+                } else {
+                    a.ULS[o + k] = u[q][s];
+                    a.WLS[o + k] = cscale(bw[q][s], a.coef[s * KS + k].qm1);
+                }
+            }
+        }
+    }
+    if (t == 0) a.dcpart[c] = dc;
+}
+
+template <class S>
+__global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
+    using US = typename Store<S>::C;
+    constexpr int T = GEN_T, KQ = GEN_KQ;
+    const int M = (int)a.M, NH = M / 2;
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *twl = lds + 2 * M;
+    const int t = threadIdx.x, c = blockIdx.x;
+    for (int m = t; m < M; m += T) twl[m] = a.tw[m];
+    const int L = a.L, s0 = c * L, e = s0 + L - 1;
+    __shared__ double lline[64];  // L <= 64 (pick_chunk)
+    if (a.pinned0 && t < L) lline[t] = a.line[s0 + t];
+    __syncthreads();
+    const int KS = a.KS;
+    const int64_t Pl = a.P, ld = a.ld;
+    const double delta = a.scal[0];
+    double pin = 0;
+    if (a.pinned0) {
+        const int nbk = pin_kblocks(a.KH);
+        for (int b = 0; b < nbk; ++b) pin += a.pinpart[b];
+    }
+    if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
+    const bool inject = a.pinned0 && a.rank == 0;
+    const bool sing = a.pinned0;
+    const double line0 = a.scal[2], line1 = a.scal[3];
+    double2 cu[KQ][2], w[KQ][2];
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) {
+        const int k = t + q * T;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            cu[q][s] = make_double2(0, 0);
+            w[q][s] = make_double2(0, 0);
+            if (k < NH) {
+                if (k == 0) {
+                    double2 c0 = make_double2(0, 0), w0 = make_double2(0, 0), cN, wN;
+                    if (!(s == 0 && sing)) chunk_carry(a, s, 0, c, delta, inject, c0, w0);
+                    chunk_carry(a, s, NH, c, delta, inject, cN, wN);
+                    cu[q][s] = make_double2(c0.x, cN.x);
+                    w[q][s] = make_double2(w0.x, wN.x);
+                } else {
+                    chunk_carry(a, s, k, c, delta, inject, cu[q][s], w[q][s]);
+                }
+            }
+        }
+    }
+    for (int j = s0; j <= e; ++j) {
+        const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) {
+            const int k = t + q * T;
+            if (k < NH) {
+                if (k == 0) {
+                    double x0[2], xN[2];
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int o0 = s * KS, oN = s * KS + NH;
+                        double ul0 = d2(Urow[o0]).x, ulN = d2(Urow[oN]).x;
+                        if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
+                            ul0 += a.ccs[o0] * delta;
+                            ulN += a.ccs[oN] * delta;
+                        }
+                        const double2 r0 = a.crr[o0], rN = a.crr[oN];
+                        const double wx = r0.x * w[q][s].x + (ul0 + cu[q][s].x);
+                        const double wy = rN.x * w[q][s].y + (ulN + cu[q][s].y);
+                        w[q][s] = make_double2(wx, wy);
+                        cu[q][s] = make_double2(cu[q][s].x * r0.y, cu[q][s].y * rN.y);
+                        x0[s] = (s == 0 && sing) ? (line0 + (double)j * line1) + lline[j - s0] : wx;
+                        xN[s] = wy;
+                    }
+                    b0[0] = make_double2(x0[0], x0[1]);
+                    b0[NH] = make_double2(xN[0], xN[1]);
+                } else {
+                    double2 X[2];
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int o = s * KS + k;
+                        double2 ul = d2(Urow[o]);
+                        if (s == 0 && inject && j == 0) ul.x += a.ccs[o] * delta;
+                        const double2 rr = a.crr[o];
+                        w[q][s] = cfma(rr.x, w[q][s], cadd(ul, cu[q][s]));
+                        cu[q][s] = cscale(cu[q][s], rr.y);
+                        X[s] = w[q][s];
+                    }
+                    b0[k] = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
+                    b0[M - k] = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
+                }
+            }
+        }
+        __syncthreads();
+        S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
+        S *row1 = out1 + (size_t)(j + 1) * ld;
+        S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
+        S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
+        S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
+        for (int i = t; i < M; i += T) {
+            const double2 z = dft_at<true>(b0, twl, M, i);
+            const double x1 = z.x - pin, x2 = z.y;
+            store_row_with_ghosts(row1, grow1, M, i, (S)(a.pin_out[0] * x1 + a.pin_out[1] * x2));
+            if (row2) store_row_with_ghosts(row2, grow2, M, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
+        }
+        __syncthreads();  // the next row's recurrence writes b0
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
 template <int N, class S>
@@ -729,12 +953,31 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
         case 2048: return launch_pass<2048>(passB, a, s);
         case 4096: return launch_pass<4096>(passB, a, s);
         case 8192: return launch_pass<8192>(passB, a, s);
-        default: return QG_ERR_UNSUPPORTED;
+        default: break;
     }
+    if (a.M % 2 != 0 || a.M > GEN_MMAX) return QG_ERR_UNSUPPORTED;
+    const size_t lds = sizeof(double2) * 3 * (size_t)a.M;  // row, transform, twiddles
+    auto go = [&](const void *fn, auto kernel) -> int {
+        QG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        kernel<<<a.Nc, GEN_T, lds, s>>>(a);
+        return QG_OK;
+    };
+    if (passB) {
+        QG_CHECK(a.f32 ? go((const void *)spec_passB_gen<float>, spec_passB_gen<float>)
+                       : go((const void *)spec_passB_gen<double>, spec_passB_gen<double>));
+    } else {
+        QG_CHECK(a.f32 ? go((const void *)spec_passA_gen<float>, spec_passA_gen<float>)
+                       : go((const void *)spec_passA_gen<double>, spec_passA_gen<double>));
+    }
+    QG_LAUNCH_CHECK();
+    return QG_OK;
 }
 
+// power-of-two rows 8 .. 8192 (FFT passes), or even rows 4 .. GEN_MMAX (direct DFT passes)
 bool SpectralSolver::supports(int64_t M, int64_t P) {
-    return M >= 8 && M <= 8192 && (M & (M - 1)) == 0 && P >= 2;
+    if (P < 2) return false;
+    if (M >= 8 && M <= 8192 && (M & (M - 1)) == 0) return true;
+    return M >= 4 && M <= GEN_MMAX && M % 2 == 0;
 }
 
 // Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic), small

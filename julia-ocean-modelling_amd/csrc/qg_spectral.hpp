@@ -31,7 +31,7 @@ struct Coef {  // per (system, k); see SpectralSolver::init
 };
 
 struct SpecArgs {
-    int64_t M, P, ld;         // M = row length (power of two), P = local rows, ld = M + 2
+    int64_t M, P, ld;         // M = row length (2^k, or even <= 2048), P = local rows, ld = M + 2
     int64_t P_total;          // global rows
     int rank, nranks;
     int L, Nc, KH, KS;        // chunk rows, chunks, M/2+1, padded k stride

@@ -44,14 +44,42 @@ def test_chunk_size_does_not_change_the_answer(env):
 
 
 def test_non_power_of_two_rows(env):
+    """Even M that is not a power of two: the spectral solver's direct-DFT passes; odd M:
+    refused by the spectral solver, plain CG instead."""
     qg, O, R = env
     m = qg.bench_model(48, P=40)
-    with pytest.raises(qg.QGError) as e:  # the spectral solver needs M = 2^k
+    st = qg.run_model_no_output(m, nsteps=5)
+    ref = O.State(R.bench_model(48, P=40)).run(5)
+    for n in ("psi", "zeta"):
+        assert rel(st.to_numpy(n), getattr(ref, n)) < TOL, n
+    pc = qg.run_model_no_output(m, nsteps=5, solver=1)  # PCG, spectral preconditioner
+    assert rel(pc.to_numpy("psi"), ref.psi) < TOL
+    m = qg.bench_model(45, P=40)
+    with pytest.raises(qg.QGError) as e:  # odd rows: no spectral solver
         qg.State(m)
     assert e.value.status == -2
     st = qg.run_model_no_output(m, nsteps=3, solver=1, precond=0, pcg_maxit=2000)
-    ref = O.State(R.bench_model(48, P=40)).run(3)
+    ref = O.State(R.bench_model(45, P=40)).run(3)
     assert rel(st.to_numpy("psi"), ref.psi) < 1e-8  # plain CG, stagnation floor ~1e-10 relres
+
+
+@pytest.mark.parametrize("M", list(range(8, 129, 8)))
+def test_reference_benchmark_sweep_sizes(env, M):
+    """The grid sweep of the reference's own benchmark, M = P = 8:8:128
+    (src/benchmarking/julia_bench_parts.jl:19), 10 steps at its dt = 30 min."""
+    qg, O, R = env
+    st = qg.run_model_no_output(qg.bench_model(M), nsteps=10)
+    ref = O.State(R.bench_model(M)).run(10)
+    for n in ("psi", "zeta"):
+        assert rel(st.to_numpy(n), getattr(ref, n)) < TOL, (n, M)
+
+
+def test_generic_rows_wide(env):
+    """The widest generic row (M = 2000, even, not 2^k) and a rectangular slab."""
+    qg, O, R = env
+    st = qg.run_model_no_output(qg.bench_model(2000, P=24, dt=600.0), nsteps=3)
+    ref = O.State(R.bench_model(2000, P=24, dt=600.0)).run(3)
+    assert rel(st.to_numpy("psi"), ref.psi) < TOL
 
 
 def test_invalid_arguments_are_refused(env):

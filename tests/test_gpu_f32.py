@@ -31,7 +31,7 @@ def env():
     return torch, qgamd, qg_oracle, qg_ref
 
 
-@pytest.mark.parametrize("N,P,steps", [(64, 64, 10), (256, 128, 10), (1024, 64, 6), (8192, 16, 3)])
+@pytest.mark.parametrize("N,P,steps", [(64, 64, 10), (256, 128, 10), (1024, 64, 6), (8192, 16, 3), (120, 72, 6)])
 def test_f32_against_f64_oracle(env, N, P, steps):
     torch, qg, O, R = env
     m = qg.bench_model(N, P=P, dt=60.0)
