@@ -695,9 +695,9 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 }
 
 // ------------------------------------------------------------------------------------
-// Generic rows (M even, not a power of two, M <= GEN_MMAX): the same passes with the row
+// Generic rows (M not a power of two, M <= GEN_MMAX, odd or even): the same passes with the row
 // transform done as a direct DFT in LDS (O(M^2) per row instead of the FFT) -- for the
-// reference's own grid sweeps (julia_bench_parts.jl:19, M = 8:8:128) and any other even M.
+// reference's own grid sweeps (julia_bench_parts.jl:19, M = 8:8:128) and any other M.
 // Everything else (recurrences, chunk summaries, carries, pin, multi-rank closure) is the
 // power-of-two code's, with the row length at run time.
 // ------------------------------------------------------------------------------------
@@ -725,6 +725,9 @@ __global__ __launch_bounds__(GEN_T) void spec_passA_gen(SpecArgs a) {
     using US = typename Store<S>::C;
     constexpr int T = GEN_T, KQ = GEN_KQ;
     const int M = (int)a.M, NH = M / 2;
+    // even M: slot k = 0 also carries the real line k = M/2; odd M: k = NH is a complex line
+    const bool odd = M & 1;
+    const int KC = odd ? NH + 1 : NH;  // slots k in [0, KC)
     extern __shared__ double2 lds[];
     double2 *b0 = lds, *b1 = lds + M, *twl = lds + 2 * M;
     const int t = threadIdx.x, c = blockIdx.x;
@@ -756,10 +759,10 @@ __global__ __launch_bounds__(GEN_T) void spec_passA_gen(SpecArgs a) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
-            if (k < NH) {
+            if (k < KC) {
                 const double2 Zk = b1[k];
-                if (k == 0) {  // the two real lines k = 0 and k = M/2
-                    const double2 Zn = b1[NH];
+                if (k == 0) {  // the two real lines k = 0 and k = M/2 (odd M: k = 0 only)
+                    const double2 Zn = odd ? make_double2(0, 0) : b1[NH];
                     dc += Zk.x;
                     a.hline[j] = Zk.x;
                     const double2 B[2] = {make_double2(Zk.x, Zn.x), make_double2(Zk.y, Zn.y)};
@@ -770,7 +773,7 @@ __global__ __launch_bounds__(GEN_T) void spec_passA_gen(SpecArgs a) {
                         u[q][s] = make_double2(a.ccs[o0] * B[s].x + r0.x * u[q][s].x,
                                                a.ccs[oN] * B[s].y + rN.x * u[q][s].y);
                         Urow[s * KS] = Store<S>::c(make_double2(u[q][s].x, 0));
-                        Urow[s * KS + NH] = Store<S>::c(make_double2(u[q][s].y, 0));
+                        if (!odd) Urow[s * KS + NH] = Store<S>::c(make_double2(u[q][s].y, 0));
                         bw[q][s] = make_double2(bw[q][s].x * r0.y + u[q][s].x, bw[q][s].y * rN.y + u[q][s].y);
                     }
                 } else {
@@ -793,16 +796,18 @@ __global__ __launch_bounds__(GEN_T) void spec_passA_gen(SpecArgs a) {
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
         const int k = t + q * T;
-        if (k < NH) {
+        if (k < KC) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const size_t o = ((size_t)c * 2 + s) * KS;
                 if (k == 0) {
                     const double q0 = a.coef[s * KS].qm1, qN = a.coef[s * KS + NH].qm1;
                     a.ULS[o] = make_double2(u[q][s].x, 0);
-                    a.ULS[o + NH] = make_double2(u[q][s].y, 0);
                     a.WLS[o] = make_double2(bw[q][s].x * q0, 0);
-                    a.WLS[o + NH] = make_double2(bw[q][s].y * qN, 0);
+                    if (!odd) {
+                        a.ULS[o + NH] = make_double2(u[q][s].y, 0);
+                        a.WLS[o + NH] = make_double2(bw[q][s].y * qN, 0);
+                    }
                 } else {
                     a.ULS[o + k] = u[q][s];
                     a.WLS[o + k] = cscale(bw[q][s], a.coef[s * KS + k].qm1);
@@ -818,6 +823,8 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
     using US = typename Store<S>::C;
     constexpr int T = GEN_T, KQ = GEN_KQ;
     const int M = (int)a.M, NH = M / 2;
+    const bool odd = M & 1;
+    const int KC = odd ? NH + 1 : NH;  // (see spec_passA_gen)
     extern __shared__ double2 lds[];
     double2 *b0 = lds, *twl = lds + 2 * M;
     const int t = threadIdx.x, c = blockIdx.x;
@@ -846,11 +853,11 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
         for (int s = 0; s < 2; ++s) {
             cu[q][s] = make_double2(0, 0);
             w[q][s] = make_double2(0, 0);
-            if (k < NH) {
+            if (k < KC) {
                 if (k == 0) {
-                    double2 c0 = make_double2(0, 0), w0 = make_double2(0, 0), cN, wN;
+                    double2 c0 = make_double2(0, 0), w0 = make_double2(0, 0), cN = c0, wN = c0;
                     if (!(s == 0 && sing)) chunk_carry(a, s, 0, c, delta, inject, c0, w0);
-                    chunk_carry(a, s, NH, c, delta, inject, cN, wN);
+                    if (!odd) chunk_carry(a, s, NH, c, delta, inject, cN, wN);
                     cu[q][s] = make_double2(c0.x, cN.x);
                     w[q][s] = make_double2(w0.x, wN.x);
                 } else {
@@ -864,13 +871,13 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
-            if (k < NH) {
+            if (k < KC) {
                 if (k == 0) {
                     double x0[2], xN[2];
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int o0 = s * KS, oN = s * KS + NH;
-                        double ul0 = d2(Urow[o0]).x, ulN = d2(Urow[oN]).x;
+                        double ul0 = d2(Urow[o0]).x, ulN = odd ? 0.0 : d2(Urow[oN]).x;
                         if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
                             ul0 += a.ccs[o0] * delta;
                             ulN += a.ccs[oN] * delta;
@@ -884,7 +891,7 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
                         xN[s] = wy;
                     }
                     b0[0] = make_double2(x0[0], x0[1]);
-                    b0[NH] = make_double2(xN[0], xN[1]);
+                    if (!odd) b0[NH] = make_double2(xN[0], xN[1]);
                 } else {
                     double2 X[2];
 #pragma unroll
@@ -955,7 +962,7 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
         case 8192: return launch_pass<8192>(passB, a, s);
         default: break;
     }
-    if (a.M % 2 != 0 || a.M > GEN_MMAX) return QG_ERR_UNSUPPORTED;
+    if (a.M > GEN_MMAX) return QG_ERR_UNSUPPORTED;
     const size_t lds = sizeof(double2) * 3 * (size_t)a.M;  // row, transform, twiddles
     auto go = [&](const void *fn, auto kernel) -> int {
         QG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -973,11 +980,11 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
     return QG_OK;
 }
 
-// power-of-two rows 8 .. 8192 (FFT passes), or even rows 4 .. GEN_MMAX (direct DFT passes)
+// power-of-two rows 8 .. 8192 (FFT passes), or any other rows 3 .. GEN_MMAX (direct DFT passes)
 bool SpectralSolver::supports(int64_t M, int64_t P) {
     if (P < 2) return false;
     if (M >= 8 && M <= 8192 && (M & (M - 1)) == 0) return true;
-    return M >= 4 && M <= GEN_MMAX && M % 2 == 0;
+    return M >= 3 && M <= GEN_MMAX;
 }
 
 // Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic), small

@@ -43,24 +43,21 @@ def test_chunk_size_does_not_change_the_answer(env):
     assert rel(a, b) < 1e-12
 
 
-def test_non_power_of_two_rows(env):
-    """Even M that is not a power of two: the spectral solver's direct-DFT passes; odd M:
-    refused by the spectral solver, plain CG instead."""
+@pytest.mark.parametrize("M,P", [(48, 40), (45, 40), (3, 8), (5, 6), (9, 12), (127, 64), (250, 30)])
+def test_non_power_of_two_rows(env, M, P):
+    """Rows that are not a power of two (even and odd): the spectral solver's direct-DFT
+    passes; also as the PCG preconditioner, and plain CG for comparison."""
     qg, O, R = env
-    m = qg.bench_model(48, P=40)
+    m = qg.bench_model(M, P=P)
     st = qg.run_model_no_output(m, nsteps=5)
-    ref = O.State(R.bench_model(48, P=40)).run(5)
+    ref = O.State(R.bench_model(M, P=P)).run(5)
     for n in ("psi", "zeta"):
         assert rel(st.to_numpy(n), getattr(ref, n)) < TOL, n
     pc = qg.run_model_no_output(m, nsteps=5, solver=1)  # PCG, spectral preconditioner
     assert rel(pc.to_numpy("psi"), ref.psi) < TOL
-    m = qg.bench_model(45, P=40)
-    with pytest.raises(qg.QGError) as e:  # odd rows: no spectral solver
-        qg.State(m)
-    assert e.value.status == -2
-    st = qg.run_model_no_output(m, nsteps=3, solver=1, precond=0, pcg_maxit=2000)
-    ref = O.State(R.bench_model(45, P=40)).run(3)
-    assert rel(st.to_numpy("psi"), ref.psi) < 1e-8  # plain CG, stagnation floor ~1e-10 relres
+    if M == 45:
+        cg = qg.run_model_no_output(m, nsteps=5, solver=1, precond=0, pcg_maxit=2000)
+        assert rel(cg.to_numpy("psi"), ref.psi) < 1e-8  # plain CG, stagnation floor ~1e-10 relres
 
 
 @pytest.mark.parametrize("M", list(range(8, 129, 8)))
@@ -75,11 +72,16 @@ def test_reference_benchmark_sweep_sizes(env, M):
 
 
 def test_generic_rows_wide(env):
-    """The widest generic row (M = 2000, even, not 2^k) and a rectangular slab."""
+    """Wide generic rows (M = 2000 even, 1999 odd; not 2^k) on rectangular slabs, and M
+    above the generic limit refused."""
     qg, O, R = env
-    st = qg.run_model_no_output(qg.bench_model(2000, P=24, dt=600.0), nsteps=3)
-    ref = O.State(R.bench_model(2000, P=24, dt=600.0)).run(3)
-    assert rel(st.to_numpy("psi"), ref.psi) < TOL
+    for M in (2000, 1999):
+        st = qg.run_model_no_output(qg.bench_model(M, P=24, dt=600.0), nsteps=3)
+        ref = O.State(R.bench_model(M, P=24, dt=600.0)).run(3)
+        assert rel(st.to_numpy("psi"), ref.psi) < TOL, M
+    with pytest.raises(qg.QGError) as e:
+        qg.State(qg.bench_model(3000, P=8))
+    assert e.value.status == -2
 
 
 def test_invalid_arguments_are_refused(env):
