@@ -71,6 +71,9 @@ __device__ __forceinline__ void store_with_ghosts(T *out, int64_t ld, int64_t M,
 template <class T>
 __device__ __forceinline__ void store_row_with_ghosts(T *row, T *grow, int M, int i, T v) {
     row[i + 1] = v;
+#ifdef QG_EXP_NOGHOST  // timing experiment only (wrong results)
+    return;
+#endif
     if (i == M - 1) row[0] = v;
     if (i == 0) row[M + 1] = v;
     if (grow) {
