@@ -699,14 +699,16 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 
 // ------------------------------------------------------------------------------------
 // Generic rows (M not a power of two, M <= GEN_MMAX, odd or even): the same passes with the row
-// transform done as a direct DFT in LDS (O(M^2) per row instead of the FFT) -- for the
-// reference's own grid sweeps (julia_bench_parts.jl:19, M = 8:8:128) and any other M.
-// Everything else (recurrences, chunk summaries, carries, pin, multi-rank closure) is the
-// power-of-two code's, with the row length at run time.
+// transform as a run-time mixed-radix Stockham FFT in LDS (radices 8, 4, 2 and the odd primes
+// up to 13, planned on the host), or, when M has a larger prime factor, a direct DFT (O(M^2)
+// per row) -- for the reference's own grid sweeps (julia_bench_parts.jl:19, M = 8:8:128) and
+// any other M.  Everything else (recurrences, chunk summaries, carries, pin, multi-rank
+// closure) is the power-of-two code's, with the row length at run time.
 // ------------------------------------------------------------------------------------
 constexpr int GEN_T = 256;
-constexpr int GEN_MMAX = 2048;
-constexpr int GEN_KQ = GEN_MMAX / 2 / GEN_T;  // wavenumber slots per thread
+constexpr int GEN_MMAX = 3200;                               // 3 row buffers of M complex in LDS
+constexpr int GEN_KQ = (GEN_MMAX / 2 + GEN_T) / GEN_T;       // wavenumber slots per thread
+constexpr int GEN_RMAX = 13;                                 // largest radix of a planned pass
 
 // X_k = sum_x src[x] W^(k x), W = tw[1] (forward) or its conjugate (inverse)
 template <bool INV>
@@ -721,6 +723,81 @@ __device__ __forceinline__ double2 dft_at(const double2 *src, const double2 *twl
         if (m >= M) m -= M;
     }
     return acc;
+}
+
+// One row transform by the planned passes a.rad[0..nrad): Stockham autosort between src and
+// dst (one barrier per pass), twiddles and the radix-R DFT from the M-entry table twl
+// (W^m = twl[m mod M], conjugated for the inverse).  Returns the buffer holding the result.
+template <bool INV>
+__device__ double2 *gen_fft(double2 *src, double2 *dst, const double2 *twl, const SpecArgs &a, int M) {
+    const int t = threadIdx.x;
+    int NS = 1;
+    for (int p = 0; p < a.nrad; ++p) {
+        const int R = a.rad[p], NB = M / R;
+        const int tstep = M / (NS * R), rstep = NB;  // W_{NS R} = twl[tstep], W_R = twl[rstep]
+        for (int b = t; b < NB; b += GEN_T) {
+            const int k = b % NS;
+            double2 v[GEN_RMAX];
+#pragma unroll
+            for (int r = 0; r < GEN_RMAX; ++r)
+                if (r < R) v[r] = src[b + r * NB];
+            if (NS > 1) {
+                int m = 0;
+                const int step = k * tstep;  // < M
+#pragma unroll
+                for (int r = 1; r < GEN_RMAX; ++r)
+                    if (r < R) {
+                        m += step;
+                        if (m >= M) m -= M;
+                        double2 w = twl[m];
+                        if (INV) w.y = -w.y;
+                        v[r] = cmul(v[r], w);
+                    }
+            }
+            const int base = (b / NS) * NS * R + k;
+            if (R == 8 || R == 4 || R == 2) {
+                if (R == 8) {
+                    double2 u[8];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) u[r] = v[r];
+                    dft8<INV>(u);
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) dst[base + r * NS] = u[r];
+                } else if (R == 4) {
+                    dft4<INV>(v[0], v[1], v[2], v[3]);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) dst[base + r * NS] = v[r];
+                } else {
+                    dft2<INV>(v[0], v[1]);
+                    dst[base] = v[0];
+                    dst[base + NS] = v[1];
+                }
+            } else {  // odd prime radix: direct R-point DFT, W_R^(q r) from the table
+#pragma unroll
+                for (int q = 0; q < GEN_RMAX; ++q)
+                    if (q < R) {
+                        double2 acc = v[0];
+                        int e = 0;  // q r mod R
+#pragma unroll
+                        for (int r = 1; r < GEN_RMAX; ++r)
+                            if (r < R) {
+                                e += q;
+                                if (e >= R) e -= R;
+                                double2 w = twl[e * rstep];
+                                if (INV) w.y = -w.y;
+                                acc = cadd(acc, cmul(v[r], w));
+                            }
+                        dst[base + q * NS] = acc;
+                    }
+            }
+        }
+        __syncthreads();
+        double2 *x = src;
+        src = dst;
+        dst = x;
+        NS *= R;
+    }
+    return src;
 }
 
 template <class S>
@@ -756,16 +833,21 @@ __global__ __launch_bounds__(GEN_T) void spec_passA_gen(SpecArgs a) {
             b0[i] = make_double2(p0 * z1 + p1 * z2, p2 * z1 + p3 * z2);
         }
         __syncthreads();
-        for (int k = t; k < M; k += T) b1[k] = dft_at<false>(b0, twl, M, k);
-        __syncthreads();
+        const double2 *Zb = b1;
+        if (a.nrad > 0) {
+            Zb = gen_fft<false>(b0, b1, twl, a, M);
+        } else {
+            for (int k = t; k < M; k += T) b1[k] = dft_at<false>(b0, twl, M, k);
+            __syncthreads();
+        }
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
             const int k = t + q * T;
             if (k < KC) {
-                const double2 Zk = b1[k];
+                const double2 Zk = Zb[k];
                 if (k == 0) {  // the two real lines k = 0 and k = M/2 (odd M: k = 0 only)
-                    const double2 Zn = odd ? make_double2(0, 0) : b1[NH];
+                    const double2 Zn = odd ? make_double2(0, 0) : Zb[NH];
                     dc += Zk.x;
                     a.hline[j] = Zk.x;
                     const double2 B[2] = {make_double2(Zk.x, Zn.x), make_double2(Zk.y, Zn.y)};
@@ -780,7 +862,7 @@ __global__ __launch_bounds__(GEN_T) void spec_passA_gen(SpecArgs a) {
                         bw[q][s] = make_double2(bw[q][s].x * r0.y + u[q][s].x, bw[q][s].y * rN.y + u[q][s].y);
                     }
                 } else {
-                    const double2 Zm = b1[M - k];
+                    const double2 Zm = Zb[M - k];
                     const double2 B[2] = {make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5),
                                           make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5)};
 #pragma unroll
@@ -829,7 +911,7 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
     const bool odd = M & 1;
     const int KC = odd ? NH + 1 : NH;  // (see spec_passA_gen)
     extern __shared__ double2 lds[];
-    double2 *b0 = lds, *twl = lds + 2 * M;
+    double2 *b0 = lds, *b1 = lds + M, *twl = lds + 2 * M;
     const int t = threadIdx.x, c = blockIdx.x;
     for (int m = t; m < M; m += T) twl[m] = a.tw[m];
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
@@ -918,8 +1000,9 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
         S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
         S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
         S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
+        const double2 *Xb = a.nrad > 0 ? gen_fft<true>(b0, b1, twl, a, M) : nullptr;
         for (int i = t; i < M; i += T) {
-            const double2 z = dft_at<true>(b0, twl, M, i);
+            const double2 z = Xb ? Xb[i] : dft_at<true>(b0, twl, M, i);
             const double x1 = z.x - pin, x2 = z.y;
             store_row_with_ghosts(row1, grow1, M, i, (S)(a.pin_out[0] * x1 + a.pin_out[1] * x2));
             if (row2) store_row_with_ghosts(row2, grow2, M, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
@@ -983,7 +1066,7 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
     return QG_OK;
 }
 
-// power-of-two rows 8 .. 8192 (FFT passes), or any other rows 3 .. GEN_MMAX (direct DFT passes)
+// power-of-two rows 8 .. 8192 (FFT passes), or any other rows 3 .. GEN_MMAX (generic passes)
 bool SpectralSolver::supports(int64_t M, int64_t P) {
     if (P < 2) return false;
     if (M >= 8 && M <= 8192 && (M & (M - 1)) == 0) return true;
@@ -1022,6 +1105,22 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.f32 = f32;
     a.KH = (int)(M / 2 + 1);
     a.KS = (a.KH + 63) & ~63;
+    a.nrad = 0;
+    // generic rows: mixed-radix plan, or none (direct DFT: rows with a prime factor > 13, and
+    // short rows, where the direct DFT measured no slower -- 120^2: 15 600-17 200 vs 15 000 steps/s)
+    if ((M & (M - 1)) != 0 && M > 128) {
+        int64_t m = M, n = 0;
+        int rad[16];
+        while (m % 8 == 0) { rad[n++] = 8; m /= 8; }
+        if (m % 4 == 0) { rad[n++] = 4; m /= 4; }
+        if (m % 2 == 0) { rad[n++] = 2; m /= 2; }
+        for (int p = 3; p <= GEN_RMAX && m > 1; p += 2)
+            while (m % p == 0 && n < 16) { rad[n++] = p; m /= p; }
+        if (m == 1) {
+            a.nrad = (int)n;
+            for (int i = 0; i < n; ++i) a.rad[i] = rad[i];
+        }
+    }
     a.dx = dx;
     a.pinned0 = pinned0 ? 1 : 0;
     std::memcpy(a.pin_in, pin_in, sizeof(a.pin_in));

@@ -61,6 +61,7 @@ struct SpecArgs {
     double *pinpart;          // per-workgroup parts of the pin value (spec_pin -> pass B)
     const double2 *cct1;      // [Nc][2][KS] chunk factors of pass B's carry-in (see chunk_carry)
     const double2 *cct2;
+    int nrad, rad[16];        // generic rows: mixed-radix pass plan (0 = direct DFT)
 };
 
 // record layout (doubles)

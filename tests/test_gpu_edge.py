@@ -43,7 +43,8 @@ def test_chunk_size_does_not_change_the_answer(env):
     assert rel(a, b) < 1e-12
 
 
-@pytest.mark.parametrize("M,P", [(48, 40), (45, 40), (3, 8), (5, 6), (9, 12), (127, 64), (250, 30)])
+@pytest.mark.parametrize("M,P", [(48, 40), (45, 40), (3, 8), (5, 6), (9, 12), (127, 64), (250, 30), (1001, 16),
+                                 (2 * 3 * 5 * 7 * 11, 12), (13 * 16, 24), (17 * 4, 20)])
 def test_non_power_of_two_rows(env, M, P):
     """Rows that are not a power of two (even and odd): the spectral solver's direct-DFT
     passes; also as the PCG preconditioner, and plain CG for comparison."""
@@ -72,15 +73,15 @@ def test_reference_benchmark_sweep_sizes(env, M):
 
 
 def test_generic_rows_wide(env):
-    """Wide generic rows (M = 2000 even, 1999 odd; not 2^k) on rectangular slabs, and M
-    above the generic limit refused."""
+    """Wide generic rows on rectangular slabs: M = 2000 and 3000 (mixed-radix passes), 1999
+    (prime: direct DFT); M above the generic limit (3200) refused."""
     qg, O, R = env
-    for M in (2000, 1999):
+    for M in (2000, 1999, 3000):
         st = qg.run_model_no_output(qg.bench_model(M, P=24, dt=600.0), nsteps=3)
         ref = O.State(R.bench_model(M, P=24, dt=600.0)).run(3)
         assert rel(st.to_numpy("psi"), ref.psi) < TOL, M
     with pytest.raises(qg.QGError) as e:
-        qg.State(qg.bench_model(3000, P=8))
+        qg.State(qg.bench_model(4000, P=8))
     assert e.value.status == -2
 
 
