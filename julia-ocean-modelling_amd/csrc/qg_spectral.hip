@@ -537,15 +537,16 @@ __device__ __forceinline__ void chunk_carry(const SpecArgs &a, int s, int k, int
     return;
 #endif
 
-    // chunk factors (host tables, constant over steps): cct1 = (q, q r^((Nc-1-c) L)),
-    // cct2 = (g_c, r^(c L)) with g_c = r^(P-n+1) (1 - r^(2n)) / (1 - r^2), n = c L
-    const size_t o = ((size_t)c * 2 + s) * a.KS + k;
-    const double2 f1 = a.cct1[o], f2 = a.cct2[o];
+    const Coef cf = a.coef[s * a.KS + k];
     const double2 Ue = a.EXT[(size_t)s * a.KS + k], We = a.EXT[(size_t)(2 + s) * a.KS + k];
-    cu = cfma(f1.y, Ue, cscale(a.UIN[o], f1.x));
-    double2 wi = cfma(f2.x, Ue, a.WIN[o]);
-    wi = cfma(f2.y, We, wi);
-    if (s == 0 && inject && c >= 1) wi.x += (f2.y * a.crr[s * a.KS + k].y) * (a.ccs[s * a.KS + k] * delta);
+    const int64_t n = (int64_t)c * a.L;
+    const double2 uin = cfma(exp((double)(a.Nc - 1 - c) * a.L * cf.lr), Ue, a.UIN[((size_t)c * 2 + s) * a.KS + k]);
+    cu = cscale(uin, cf.q);
+    double gc = 0;
+    if (n > 0) gc = exp((double)(a.P - n + 1) * cf.lr) * (expm1(2.0 * n * cf.lr) / expm1(2.0 * cf.lr));
+    double2 wi = cfma(gc, Ue, a.WIN[((size_t)c * 2 + s) * a.KS + k]);
+    wi = cfma(exp((double)n * cf.lr), We, wi);
+    if (s == 0 && inject && c >= 1) wi.x += exp((double)(n - 1) * cf.lr) * (cf.cs * delta);
     w = wi;
 }
 
@@ -1135,7 +1136,6 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
         tw[m] = make_double2((double)cosl(ang), (double)-sinl(ang));
     }
     std::vector<Coef> coef(2 * (size_t)KS);
-    std::vector<long double> lrl(2 * (size_t)KS, 0.0L);  // log r per line, for the chunk tables
     std::memset(coef.data(), 0, sizeof(Coef) * coef.size());
     for (int s = 0; s < 2; ++s)
         for (int k = 0; k < a.KH; ++k) {
@@ -1149,7 +1149,6 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
             const long double sq = sqrtl(d * (d + 2));
             const long double r = 1 / ((1 + d) + sq);
             const long double lr = -log1pl(d + sq);
-            lrl[s * KS + k] = lr;
             if (!(r > 1e-300L)) return QG_ERR_UNSUPPORTED;  // |alpha| dx^2 beyond double range
             cf.r = (double)r;
             cf.rinv = (double)(1 / r);
@@ -1178,7 +1177,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const size_t n_line = align_up(sizeof(double) * P);  // (hline and line)
     const size_t n_scal = align_up(sizeof(double) * 8);
     const size_t n_pinpart = align_up(sizeof(double) * (pin_kblocks(a.KH) + 1));
-    bytes_ = n_tw + n_coef + n_hot + n_U + 6 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart;
+    bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart;
     if (hipMalloc(&mem_, bytes_) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -1203,9 +1202,6 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.hline = (double *)take(n_line);
     a.scal = (double *)take(n_scal);
     a.pinpart = (double *)take(n_pinpart);
-    double2 *d_cct1 = (double2 *)take(n_S), *d_cct2 = (double2 *)take(n_S);
-    a.cct1 = d_cct1;
-    a.cct2 = d_cct2;
     a.tw = d_tw;
     a.coef = d_coef;
     QG_HIP(hipMemcpy(d_tw, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice));
@@ -1220,29 +1216,6 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
         QG_HIP(hipMemcpy(d_hot, hot.data(), sizeof(double) * hot.size(), hipMemcpyHostToDevice));
         a.crr = reinterpret_cast<const double2 *>(d_hot);
         a.ccs = d_hot + 4 * KS;
-    }
-    {  // chunk factors of chunk_carry (pass B prologue), long double -> double
-        std::vector<double2> t1((size_t)a.Nc * 2 * KS), t2((size_t)a.Nc * 2 * KS);
-        for (int c = 0; c < a.Nc; ++c)
-            for (int s = 0; s < 2; ++s)
-                for (int k = 0; k < KS; ++k) {
-                    const size_t o = ((size_t)c * 2 + s) * KS + k;
-                    const long double lr = lrl[s * KS + k];
-                    const bool line = k < a.KH && !(s == 0 && pinned0 && k == 0);
-                    if (!line) {
-                        t1[o] = t2[o] = make_double2(0, 0);
-                        continue;
-                    }
-                    const long double n = (long double)c * L;
-                    const long double q = expl(L * lr);
-                    const long double e1 = expl((long double)(a.Nc - 1 - c) * L * lr);
-                    const long double gc = c == 0 ? 0.0L : expl(((long double)P - n + 1) * lr) *
-                                                               (expm1l(2 * n * lr) / expm1l(2 * lr));
-                    t1[o] = make_double2((double)q, (double)(q * e1));
-                    t2[o] = make_double2((double)gc, (double)expl(n * lr));
-                }
-        QG_HIP(hipMemcpy(d_cct1, t1.data(), sizeof(double2) * t1.size(), hipMemcpyHostToDevice));
-        QG_HIP(hipMemcpy(d_cct2, t2.data(), sizeof(double2) * t2.size(), hipMemcpyHostToDevice));
     }
     QG_HIP(hipMemset(a.rec, 0, n_rec));
     QG_HIP(hipMemset(a.scal, 0, n_scal));

@@ -59,8 +59,6 @@ struct SpecArgs {
     double *line;             // [P] centred local part of the singular line, scaled (carry)
     double *scal;             // [0] = delta, [1] = pin, [2] [3]: singular-line offset, slope
     double *pinpart;          // per-workgroup parts of the pin value (spec_pin -> pass B)
-    const double2 *cct1;      // [Nc][2][KS] chunk factors of pass B's carry-in (see chunk_carry)
-    const double2 *cct2;
     int nrad, rad[16];        // generic rows: mixed-radix pass plan (0 = direct DFT)
 };
 
