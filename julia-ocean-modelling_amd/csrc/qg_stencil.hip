@@ -273,6 +273,240 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, i
 }
 
 // ------------------------------------------------------------------------------------
+// Float32 tendency, two points per thread (register blocking).  With F32 fields the kernel
+// above moves half the bytes but keeps its per-point LDS reads and per-row barrier, and is
+// bound by those, not by HBM.  Here each thread owns the adjacent pair
+// (x0 + 2t, x0 + 2t + 1): one 8-byte access per row and field (global and LDS), and the
+// stencil neighbours of both points come from 4-wide register windows of each ring row.
+// The arithmetic per point is tendency_kernel's, in the same order: bit-identical results.
+// All rings carry an x-halo of 2, so every pair sits at an even (8-byte aligned) LDS index.
+// ------------------------------------------------------------------------------------
+// pair types: V = 2 elements at an LDS pair (aligned to 2 elements), VU = 2 elements in a
+// field row (interior rows start at element 1: aligned to one element only)
+template <class T>
+struct PairT;
+template <>
+struct PairT<float> {
+    typedef float V __attribute__((ext_vector_type(2)));
+    typedef float VU __attribute__((ext_vector_type(2), aligned(4)));
+};
+template <>
+struct PairT<double> {
+    typedef double V __attribute__((ext_vector_type(2)));
+    typedef double VU __attribute__((ext_vector_type(2), aligned(8)));
+};
+
+// store the pair (xa, xa+1) of row j with its periodic images (store_row_with_ghosts x 2)
+template <class T>
+__device__ __forceinline__ void store_pair_with_ghosts(T *row, T *grow, int M, int xa, T v0, T v1, bool has_b) {
+    using VU = typename PairT<T>::VU;
+    auto put = [&](T *r) {
+        if (has_b) {
+            *(VU *)(r + xa + 1) = VU{v0, v1};
+            if (xa + 1 == M - 1) r[0] = v1;
+        } else {
+            r[xa + 1] = v0;
+            if (xa == M - 1) r[0] = v0;
+        }
+        if (xa == 0) r[M + 1] = v0;
+    };
+    put(row);
+    if (grow) put(grow);
+}
+
+template <int TX, class T>
+__global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int nyA, int nyB) {
+    using V = typename PairT<T>::V;
+    using VU = typename PairT<T>::VU;
+    constexpr int RP = 6, RZ = 5, RL = 4, W = 2 * TX, WL = W + 4;
+    const int layer = blockIdx.z;
+    const int t = threadIdx.x;
+    const int M = (int)a.M, P = (int)a.P;
+    const int64_t ld = a.ld;
+    const int x0 = blockIdx.x * W;
+    const int xa = x0 + 2 * t;  // own points xa, xa + 1
+    const int y = blockIdx.y;
+    const bool second = y >= nyA;
+    const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
+    const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
+    const int jb0 = r0 + (int)(((int64_t)yy * nr) / ny);
+    const int jb1 = r0 + (int)(((int64_t)(yy + 1) * nr) / ny);
+    if (jb0 >= jb1) return;  // uniform over the block
+
+    __shared__ __attribute__((aligned(16))) T sp[RP][WL];
+    __shared__ __attribute__((aligned(16))) T sz[RZ][WL];
+    __shared__ __attribute__((aligned(16))) T sl[RL][WL];
+
+    const T *psi = a.psi[layer];
+    const T *zeta = a.zeta[layer];
+    const RowSrcT<T> &prs = a.psi_rows[layer];
+    const RowSrcT<T> &zrs = a.zeta_rows[layer];
+    const T dx = (T)a.dx, idx = T(1) / dx, idx2 = idx * idx;
+    const T cdc = T(0.5) * idx;
+    const T den = T(12) * (dx * dx);
+    const T visc = (T)a.visc, dtT = (T)a.dt, Ut = (T)a.U, rt = (T)a.r;
+    const bool small = M < W + 4;
+
+    auto wx = [&](int x) -> int {
+        if (small) return ((x % M) + M) % M;
+        return x < 0 ? x + M : (x >= M ? x - M : x);
+    };
+    auto rowp = [&](const T *base, const RowSrcT<T> &rs, int j) -> const T * {
+        if (j >= 0 && j < P) return base + fidx(1, j + 1, ld);
+        return rs.halo[j < 0 ? j + 2 : (j - P) + 2];
+    };
+    const int hq = t == 0 ? 0 : (t == TX - 1 ? W + 2 : -1);  // halo pair LDS index, or none
+    const int xh = t == 0 ? x0 - 2 : x0 + W;
+    const bool has_a = xa < M, has_b = xa + 1 < M;
+    const bool ab3 = a.ab3 != 0;
+    const int c0 = 2 * t + 2;  // LDS index of xa
+
+    auto load_pair = [&](const T *r, V &c) {
+        if (has_b) {
+            const VU v = *(const VU *)(r + xa);
+            c = V{v.x, v.y};
+        } else {
+            c = V{r[wx(xa)], r[wx(xa + 1)]};
+        }
+    };
+    auto load_halo = [&](const T *r, V &h) {
+        if (hq >= 0) h = V{r[wx(xh)], r[wx(xh + 1)]};
+    };
+    V pc = {0, 0}, ph = {0, 0}, zc = {0, 0}, zh = {0, 0}, f1 = {0, 0}, f2 = {0, 0};
+    auto fetch_psi = [&](int j, V &c, V &h) {
+        const T *r = rowp(psi, prs, j);
+        load_pair(r, c);
+        load_halo(r, h);
+    };
+    auto fetch_zeta = [&](int j, V &c, V &h) {
+        const T *r = rowp(zeta, zrs, j);
+        load_pair(r, c);
+        load_halo(r, h);
+    };
+    auto fetch_f = [&](int j, V &g1, V &g2) {
+        if (ab3 && has_a) {
+            const size_t o = (size_t)(j + 1) * ld + 1;
+            const T *p1 = a.fprev1[layer] + o, *p2 = a.fprev2[layer] + o;
+            if (has_b) {
+                const VU u1 = *(const VU *)(p1 + xa), u2 = *(const VU *)(p2 + xa);
+                g1 = V{u1.x, u1.y};
+                g2 = V{u2.x, u2.y};
+            } else {
+                g1.x = p1[xa];
+                g2.x = p2[xa];
+            }
+        }
+    };
+    auto commit = [&](T *d, V c, V h) {
+        *(V *)(d + c0) = c;
+        if (hq >= 0) *(V *)(d + hq) = h;
+    };
+    auto ring = [](int j, int R) { return (j + 2 * R) % R; };
+    auto lap_row = [&](int j) {  // lap(psi) at x0-1 .. x0+W (LDS 1 .. W+2)
+        const T *pm = sp[ring(j - 1, RP)], *p0 = sp[ring(j, RP)], *pp = sp[ring(j + 1, RP)];
+        T *dst = sl[ring(j, RL)];
+        const V a0 = *(const V *)(p0 + c0 - 2), a1 = *(const V *)(p0 + c0),
+                    a2 = *(const V *)(p0 + c0 + 2);
+        const V m = *(const V *)(pm + c0), p = *(const V *)(pp + c0);
+        V r;
+        r.x = ((((a0.y + a1.y) - T(4) * a1.x) + m.x) + p.x) * idx2;
+        r.y = ((((a1.x + a2.x) - T(4) * a1.y) + m.y) + p.y) * idx2;
+        *(V *)(dst + c0) = r;
+        if (t == 0) dst[1] = ((((p0[0] + p0[2]) - T(4) * p0[1]) + pm[1]) + pp[1]) * idx2;
+        if (t == TX - 1)
+            dst[W + 2] = ((((p0[W + 1] + p0[W + 3]) - T(4) * p0[W + 2]) + pm[W + 2]) + pp[W + 2]) * idx2;
+    };
+
+    // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 straight into LDS
+    for (int j = jb0 - 2; j <= jb0 + 2; ++j) {
+        V c = {0, 0}, h = {0, 0};
+        fetch_psi(j, c, h);
+        commit(sp[ring(j, RP)], c, h);
+    }
+    for (int j = jb0 - 1; j <= jb0 + 1; ++j) {
+        V c = {0, 0}, h = {0, 0};
+        fetch_zeta(j, c, h);
+        commit(sz[ring(j, RZ)], c, h);
+    }
+    if (jb0 + 2 <= jb1) {
+        fetch_psi(jb0 + 3, pc, ph);
+        fetch_zeta(jb0 + 2, zc, zh);
+    }
+    fetch_f(jb0, f1, f2);
+    __syncthreads();
+    lap_row(jb0 - 1);
+    lap_row(jb0);
+    lap_row(jb0 + 1);
+
+    const T bl = (T)a.beta[layer];
+    T *zo = a.zeta_out[layer], *fo = a.f_out[layer];
+    const bool gr = a.write_ghost_rows;
+    for (int j = jb0; j < jb1; ++j) {
+        const bool more = j + 2 <= jb1;
+        if (more) {
+            commit(sp[ring(j + 3, RP)], pc, ph);
+            commit(sz[ring(j + 2, RZ)], zc, zh);
+        }
+        const V f1c = f1, f2c = f2;
+        if (j + 1 + 2 <= jb1) {
+            fetch_psi(j + 4, pc, ph);
+            fetch_zeta(j + 3, zc, zh);
+        }
+        if (j + 1 < jb1) fetch_f(j + 1, f1, f2);
+        __syncthreads();
+        if (more) lap_row(j + 2);
+        if (has_a) {
+            // 4-wide windows (LDS c0-1 .. c0+2) of the zeta / psi rows j-1, j, j+1 and lap row j;
+            // lap rows j-1, j+1 at the pair only
+            T Zw[3][4], Sw[3][4], L0w[4];
+            const T *zr[3] = {sz[ring(j - 1, RZ)], sz[ring(j, RZ)], sz[ring(j + 1, RZ)]};
+            const T *pr[3] = {sp[ring(j - 1, RP)], sp[ring(j, RP)], sp[ring(j + 1, RP)]};
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const V u0 = *(const V *)(zr[r] + c0 - 2), u1 = *(const V *)(zr[r] + c0),
+                            u2 = *(const V *)(zr[r] + c0 + 2);
+                Zw[r][0] = u0.y; Zw[r][1] = u1.x; Zw[r][2] = u1.y; Zw[r][3] = u2.x;
+                const V s0 = *(const V *)(pr[r] + c0 - 2), s1 = *(const V *)(pr[r] + c0),
+                            s2 = *(const V *)(pr[r] + c0 + 2);
+                Sw[r][0] = s0.y; Sw[r][1] = s1.x; Sw[r][2] = s1.y; Sw[r][3] = s2.x;
+            }
+            const T *l0 = sl[ring(j, RL)];
+            {
+                const V u0 = *(const V *)(l0 + c0 - 2), u1 = *(const V *)(l0 + c0),
+                            u2 = *(const V *)(l0 + c0 + 2);
+                L0w[0] = u0.y; L0w[1] = u1.x; L0w[2] = u1.y; L0w[3] = u2.x;
+            }
+            const V Lm = *(const V *)(sl[ring(j - 1, RL)] + c0), Lp = *(const V *)(sl[ring(j + 1, RL)] + c0);
+            T out_z[2], out_f[2];
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const int w = 1 + v;  // window index of the point
+                const T lm = v ? Lm.y : Lm.x, lp = v ? Lp.y : Lp.x;
+                const T biharm = ((((L0w[w - 1] + L0w[w + 1]) - T(4) * L0w[w]) + lm) + lp) * idx2;
+                const T v_term = visc * biharm;
+                auto Z = [&](int da, int db) { return Zw[db + 1][w + da]; };
+                auto S = [&](int da, int db) { return Sw[db + 1][w + da]; };
+                const T J_term = arakawa_point<T>(Z, S, den);
+                const T beta_term = bl * (cdc * (Sw[1][w + 1] - Sw[1][w - 1]));
+                T last;
+                if (layer == 0) last = Ut * (cdc * (Zw[1][w + 1] - Zw[1][w - 1]));
+                else last = rt * L0w[w];
+                const T F = ((v_term - J_term) - beta_term) - last;
+                const T zcen = Zw[1][w];
+                const T g1 = v ? f1c.y : f1c.x, g2 = v ? f2c.y : f2c.x;
+                out_z[v] = ab3 ? zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * g1)) + ((T)(5.0 / 12.0) * g2))
+                               : zcen + (dtT * F);
+                out_f[v] = F;
+            }
+            store_pair_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, xa, out_z[0],
+                                   out_z[1], has_b);
+            store_pair_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, xa, out_f[0],
+                                   out_f[1], has_b);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Seeded initialise_model: psi and zeta of slot 0, ghosts included, computed directly at
 // the wrapped GLOBAL index (so slabs need no communication).  model.jl:37-62.
 // ------------------------------------------------------------------------------------
@@ -388,6 +622,41 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     return QG_OK;
 }
 
+// Float32 default: the pair kernel over whole chip-fulls of 512-point strips (as above);
+// QG_TEND_PAIR=0 selects the one-point kernel instead.
+template <int TX, class T>
+static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
+    constexpr int W = 2 * TX;
+    static int sl = 0;
+    if (sl == 0) {
+        int dev = 0, cus = 0, per = 0;
+        QG_HIP(hipGetDevice(&dev));
+        QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_pair_kernel<TX, T>, TX, 0));
+        sl = cus * (per > 0 ? per : 1);
+    }
+    const char *e = std::getenv("QG_TEND_WAVES");
+    const int waves = e ? std::max(1, std::atoi(e)) : 2;
+    const int nx = (int)((a.M + W - 1) / W);
+    const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
+    const int target = std::max(1, waves * sl / (2 * nx));
+    auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
+    const int nyA = split(rA), nyB = split(rB);
+    dim3 grid((unsigned)nx, (unsigned)(nyA + nyB), 2);
+    tendency_pair_kernel<TX, T><<<grid, TX, 0, s>>>(a, nyA, nyB);
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+static bool tend_pair_enabled() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = std::getenv("QG_TEND_PAIR");
+        v = e ? std::atoi(e) : 1;
+    }
+    return v != 0;
+}
+
 // Tile/pipeline variant (tuning knob; default 0).  QG_TEND_VARIANT selects it at run time.
 static int tend_variant() {
     static int v = -1;
@@ -426,6 +695,9 @@ static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
         case 512: return launch_tend_variant<512, 1, T>(a, tr, s);
         default: break;
     }
+    if constexpr (sizeof(T) == 4) {
+        if (tend_variant() == 0 && tw == 0 && tend_pair_enabled() && a.M % 2 == 0) return launch_tend_pair<256>(a, s);
+    }  // (F64 pair kernel measured slower: 0.41-0.43 vs 0.386 ms at 4096^2 -- HBM-bound already)
     if (tend_variant() == 0 && tw == 0) {
         // ~870^2 .. ~1750^2 points: 128-wide strips of 8 rows (tile sweep: 1024^2 35 vs 38 us)
         const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
