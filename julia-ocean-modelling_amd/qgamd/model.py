@@ -183,6 +183,7 @@ class State:
                  pcg_rtol=1e-12, pcg_maxit=500, dtype=None):
         """dtype: torch.float64 (default, the reference's arithmetic) or torch.float32 (the
         F32 state of BASELINE config 5; spectral solver only)."""
+        _lib.lib()  # the HIP library first: no CPU fallback, fail before touching the device
         torch = _torch()
         self.model = m
         self.P_local = m.P if P_local is None else P_local

@@ -140,3 +140,18 @@ def test_checkpoint_format_is_checked(tmp_path):
     np.savez(bad, meta=np.array(json.dumps({"format": "something-else"})))
     with pytest.raises(ValueError):
         qgamd.read_checkpoint(str(bad))
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: without the HIP library the product path raises at first use (a
+    fresh interpreter with QGMI355_LIB pointing at nothing)."""
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import qgamd\n"
+            "try:\n"
+            "    qgamd.State(qgamd.bench_model(32))\n"
+            "except RuntimeError as e:\n"
+            "    print('RAISED', 'no CPU fallback' in str(e))\n") % PKG
+    env = dict(os.environ, QGMI355_LIB=str(tmp_path / "absent.so"))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert "RAISED True" in r.stdout, (r.stdout, r.stderr)
