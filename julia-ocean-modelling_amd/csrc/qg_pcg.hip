@@ -43,14 +43,16 @@ __device__ __forceinline__ bool is_pin(const PcgArgs &a, int64_t i, int64_t j) {
 // the matrix is zeroed (laplacian.jl:71-73) -- and an identity row of its own.  The pin's
 // four neighbours are found in global coordinates: (1,0), (M-1,0), (0,1), (0,P_total-1)
 // (the last wraps onto rank G-1's top row).  p carries a valid ghost ring.
-__device__ __forceinline__ double apply_at(const PcgArgs &a, int s, const double *p, int64_t i, int64_t j) {
+// (the field is read through val(d) = value at memory offset d from the point)
+template <class F>
+__device__ __forceinline__ double apply_f(const PcgArgs &a, int s, F val, int64_t i, int64_t j) {
     const int64_t ld = a.ld;
-    const double *c = p + fidx(i + 1, j + 1, ld);
-    double w = c[-1], e = c[1], so = c[-ld], n = c[ld];
+    const double c0 = val(0);
+    double w = val(-1), e = val(1), so = val(-ld), n = val(ld);
     if (s == 0 && a.pinned0) {
         const int64_t jg = j + a.j_offset;
         if (jg == 0) {
-            if (i == 0) return c[0];  // identity row
+            if (i == 0) return c0;  // identity row
             if (i == 1) w = 0;
             if (i == a.M - 1) e = 0;
         }
@@ -59,8 +61,13 @@ __device__ __forceinline__ double apply_at(const PcgArgs &a, int s, const double
             if (jg == a.P_total - 1) n = 0;
         }
     }
-    const double lap = ((((w + e) - 4 * c[0]) + so) + n) * a.idx2;
-    return -(lap + a.alpha[s] * c[0]);
+    const double lap = ((((w + e) - 4 * c0) + so) + n) * a.idx2;
+    return -(lap + a.alpha[s] * c0);
+}
+
+__device__ __forceinline__ double apply_at(const PcgArgs &a, int s, const double *p, int64_t i, int64_t j) {
+    const double *c = p + fidx(i + 1, j + 1, a.ld);
+    return apply_f(a, s, [&](int64_t d) { return c[d]; }, i, j);
 }
 
 // right-hand side b_s = -(proj_in zeta)_s at one point, b = 0 on the pin row (model.jl:185)
@@ -157,6 +164,49 @@ __global__ __launch_bounds__(PCG_T) void pcg_fast_finish(PcgArgs a) {
                               a.ghost_rows);
     }
     block_sumN<2>(v, a.partial);
+}
+
+// ---- certified preconditioner step (exact spectral preconditioner, invertible P_fwd) -----
+// The spectral solve writes psi = P_fwd z0 (z0 = B^-1 b) straight into the outputs; this pass
+// certifies it: z0 = P_fwd^-1 psi is re-formed at the stencil points, r0 = b - B z0 and
+// ||r0||^2, ||b||^2 per system.  Accepting x = z0 when ||r0|| <= rtol ||b|| is PCG's first
+// step with alpha = 1 (the exact preconditioner gives alpha = 1 to roundoff); otherwise the
+// general loop restarts from x0 = z0.
+__device__ __forceinline__ double z_from_out(const PcgArgs &a, int s, size_t o) {
+    return a.pinv_out[2 * s] * a.out1[o] + a.pinv_out[2 * s + 1] * a.out2[o];
+}
+
+__global__ __launch_bounds__(PCG_T) void pcg_cert_check(PcgArgs a) {
+    double v[4] = {0, 0, 0, 0};  // per system: (b,b), (r0,r0)
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        for (int s = 0; s < 2; ++s) {
+            const double b = rhs_at(a, s, i, j);
+            // pin row: the spectral pass writes the pinned unknown as exactly 0 (= b there)
+            const double r = (s == 0 && is_pin(a, i, j))
+                                 ? 0.0
+                                 : b - apply_f(a, s, [&](int64_t d) { return z_from_out(a, s, o + d); }, i, j);
+            v[2 * s] += b * b;
+            v[2 * s + 1] += r * r;
+        }
+    }
+    block_sumN<4>(v, a.partial);
+}
+
+// restart state: x0 = z0, r0 = b - B z0
+__global__ __launch_bounds__(PCG_T) void pcg_cert_restart(PcgArgs a) {
+    PCG_FOR_POINTS(a) {
+        const size_t o = fidx(i + 1, j + 1, a.ld);
+        for (int s = 0; s < 2; ++s) {
+            if (s == 0 && is_pin(a, i, j)) {  // (see pcg_cert_check)
+                a.x[s][o] = 0;
+                a.r[s][o] = 0;
+                continue;
+            }
+            a.x[s][o] = z_from_out(a, s, o);
+            a.r[s][o] = rhs_at(a, s, i, j) - apply_f(a, s, [&](int64_t d) { return z_from_out(a, s, o + d); }, i, j);
+        }
+    }
 }
 
 // fallback after a fast iteration that did not converge: the general loop's state after
@@ -273,7 +323,7 @@ __global__ __launch_bounds__(1024) void pcg_rank_sumN(PcgArgs a, int nblk) {
 }
 
 // fast-path scalars from the (gathered) sums: what 0: (b,z),(z,Bz),(b,b) -> alpha, rz, bb;
-// what 1: ||r1||^2 -> rr
+// what 1: ||r1||^2 -> rr; what 2: (b,b), (r0,r0) -> bb, rr
 __global__ void pcg_fast_scalar(PcgArgs a, int what, const double *gathered, int nv, int nranks) {
     if (threadIdx.x != 0) return;
     for (int s = 0; s < 2; ++s) {
@@ -288,9 +338,17 @@ __global__ void pcg_fast_scalar(PcgArgs a, int what, const double *gathered, int
             sc[PCG_ALPHA + s] = (zq != 0 && bz != 0) ? bz / zq : 0.0;
             sc[PCG_RZ + s] = bz;
             sc[PCG_BB + s] = bb;
-        } else {
+        } else if (what == 1) {
             double rr = 0;
             for (int g = 0; g < nranks; ++g) rr += gathered[nv * g + s];
+            sc[PCG_RR + s] = rr;
+        } else {  // what 2: certified step, (b,b), (r0,r0) per system
+            double bb = 0, rr = 0;
+            for (int g = 0; g < nranks; ++g) {
+                bb += gathered[nv * g + 2 * s];
+                rr += gathered[nv * g + 2 * s + 1];
+            }
+            sc[PCG_BB + s] = bb;
             sc[PCG_RR + s] = rr;
         }
     }
@@ -336,6 +394,17 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
     a.pinned0 = pinned0;
     std::memcpy(a.proj_in, proj_in, sizeof(a.proj_in));
     std::memcpy(a.proj_out, proj_out, sizeof(a.proj_out));
+    {  // inverse of the back-projection, for the certified step (0 = not invertible)
+        const double det = proj_out[0] * proj_out[3] - proj_out[1] * proj_out[2];
+        cert_ = det != 0 && std::isfinite(1.0 / det);
+        if (cert_) {
+            a.pinv_out[0] = proj_out[3] / det;
+            a.pinv_out[1] = -proj_out[1] / det;
+            a.pinv_out[2] = -proj_out[2] / det;
+            a.pinv_out[3] = proj_out[0] / det;
+        }
+        if (std::getenv("QG_PCG_NOCERT")) cert_ = false;  // A/B: the alpha iteration below
+    }
     rtol_ = rtol > 0 ? rtol : 1e-13;
     maxit_ = maxit > 0 ? maxit : 500;
     precond_ = precond;
@@ -435,7 +504,38 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
     relres_[0] = relres_[1] = -1;
     int status = QG_ERR_NOT_CONVERGED;
     bool resume = false;  // continue the general loop after a fast first iteration
-    if (precond_ == QG_PRECOND_SPECTRAL) {
+    int first_it = 1;
+    if (precond_ == QG_PRECOND_SPECTRAL && cert_ && out2) {
+        // psi = P_fwd z0 straight from the spectral solve, then one certification pass
+        QG_CHECK(pre_.solve(a.in1, a.in2, a.out1, a.out2, ghost_rows, s, gather, user, a.proj_in, a.proj_out));
+        if (!ghost_rows && halo) {
+            double *f[2] = {a.out1, a.out2};
+            QG_CHECK(halo(halo_user, f, 2, a.M, a.P, -1, nullptr, s));
+        }
+        pcg_cert_check<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce_fast<4>(a, nblk_, 2, gathered_, s, gather, user));
+        QG_HIP(hipMemcpyAsync(host, a.scal, sizeof(host), hipMemcpyDeviceToHost, s));
+        QG_HIP(hipStreamSynchronize(s));
+        iters_ = 1;
+        bool done = true;
+        for (int k = 0; k < 2; ++k) {
+            const double bb = host[PCG_BB + k], rr = host[PCG_RR + k];
+            relres_[k] = bb > 0 ? std::sqrt(rr / bb) : std::sqrt(rr);
+            if (!(relres_[k] <= rtol_)) done = false;
+        }
+        if (done) return QG_OK;  // psi is the certified z0
+        pcg_cert_restart<<<grid, PCG_T, 0, s>>>(a);  // x0 = z0, r0 = b - B z0; bb already set
+        QG_LAUNCH_CHECK();
+        QG_CHECK(precond());
+        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce(4, s, gather, user));
+        pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 1);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(fix_p_ghosts());
+        first_it = 2;
+    } else if (precond_ == QG_PRECOND_SPECTRAL) {
         // z0 = B^-1 b straight from zeta: B^-1 (-proj_in zeta) = A^-1 proj_in zeta, i.e. the
         // spectral solve with the model's projection (the pin row of b is irrelevant to it)
         const double id[4] = {1, 0, 0, 1};
@@ -481,7 +581,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
     // 1e-10 -- the iterate is then as accurate as the arithmetic allows.
     double prev[2] = {1e300, 1e300};
     int stall = 0;
-    for (int it = resume ? 2 : 1; it <= maxit_; ++it) {
+    for (int it = resume ? 2 : first_it; it <= maxit_; ++it) {
         if (resume) {  // z1 = M^-1 r1, beta, p1 = z1 + beta p0 (the tail of iteration 1)
             resume = false;
             prev[0] = relres_[0];

@@ -16,6 +16,7 @@ struct PcgArgs {
     double alpha[2];
     int pinned0;
     double proj_in[4], proj_out[4];
+    double pinv_out[4];  // proj_out^-1 (certified preconditioner step)
     int ghost_rows;
     const double *in1, *in2;
     double *out1, *out2;
@@ -44,6 +45,7 @@ private:
     PcgArgs a_{};
     SpectralSolver pre_;
     int precond_ = 0, maxit_ = 500, nblk_ = 0, iters_ = 0;
+    bool cert_ = false;  // proj_out invertible: the certified preconditioner step
     double rtol_ = 1e-13, relres_[2] = {-1, -1};
     void *mem_ = nullptr;
     double *gathered_ = nullptr;

@@ -679,6 +679,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         Inv::run(b0, b1, twl, xo);
         S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
         S *row1 = out1 + (size_t)(j + 1) * ld;
+        const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
         S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
         S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
         S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
@@ -689,7 +690,9 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                 double2 z;
                 if constexpr (Plan::REG_OUT) z = xo[p];
                 else z = Xb[lay<Plan::LAST_NS>(i)];
-                const double x1 = z.x - pin, x2 = z.y;
+                // the pinned unknown is exactly 0 (get_poisson_cholesky's identity row), not
+                // its value minus the spectrally computed pin (a roundoff residue)
+                const double x1 = (pin_row && i == 0) ? 0.0 : z.x - pin, x2 = z.y;
                 store_row_with_ghosts(row1, grow1, N, i, (S)(a.pin_out[0] * x1 + a.pin_out[1] * x2));
                 if (row2) store_row_with_ghosts(row2, grow2, N, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
             }
@@ -998,13 +1001,14 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
         __syncthreads();
         S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
         S *row1 = out1 + (size_t)(j + 1) * ld;
+        const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
         S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
         S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
         S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
         const double2 *Xb = a.nrad > 0 ? gen_fft<true>(b0, b1, twl, a, M) : nullptr;
         for (int i = t; i < M; i += T) {
             const double2 z = Xb ? Xb[i] : dft_at<true>(b0, twl, M, i);
-            const double x1 = z.x - pin, x2 = z.y;
+            const double x1 = (pin_row && i == 0) ? 0.0 : z.x - pin, x2 = z.y;
             store_row_with_ghosts(row1, grow1, M, i, (S)(a.pin_out[0] * x1 + a.pin_out[1] * x2));
             if (row2) store_row_with_ghosts(row2, grow2, M, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
         }

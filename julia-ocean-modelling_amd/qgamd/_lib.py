@@ -110,6 +110,12 @@ def lib():
             raise RuntimeError(
                 f"{LIB_PATH} not found: build it with `make -C julia-ocean-modelling_amd` "
                 "(or __graft_entry__.build()); the QG hot path has no CPU fallback")
+        # PyTorch first: it ships its own HIP runtime, and the library must bind to that one
+        # (loading ours first would bring in /opt/rocm's libamdhip64 as a second runtime)
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             f = getattr(L, name)

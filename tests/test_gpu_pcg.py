@@ -57,3 +57,41 @@ def test_pcg_model_run_matches_oracle(env, M, P, precond):
     psi = st.to_numpy("psi")
     tol = 1e-10 if precond else 1e-8
     assert np.linalg.norm(psi - ref.psi) / np.linalg.norm(ref.psi) < tol
+
+
+def test_certified_preconditioner_step(env):
+    """Exact spectral preconditioner: the spectral solve writes psi = P_fwd z0 and one pass
+    certifies ||b - B z0|| / ||b|| <= rtol -- one iteration per step, residual at roundoff."""
+    torch, qg, R, O = env
+    st = qg.initialise_model(qg.bench_model(64), solver=1)
+    for t in range(1, 9):
+        st.step(t)
+        s = st.stats()
+        assert s["iters"][0] == 1 and max(s["relres"]) < 1e-13, s
+    ref = O.State(R.bench_model(64)).run(8)
+    assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-10
+
+
+def test_certification_failure_restarts_from_z0(env):
+    """A residual target below the roundoff floor: the certification fails, the general loop
+    restarts from x0 = z0 and stops at its stagnation floor; the answer is unchanged."""
+    torch, qg, R, O = env
+    st = qg.initialise_model(qg.bench_model(64, P=48), solver=1, pcg_rtol=1e-30, pcg_maxit=50)
+    for t in range(1, 5):
+        st.step(t)
+        s = st.stats()
+        assert s["iters"][0] >= 2 and max(s["relres"]) <= 1e-10, s
+    ref = O.State(R.bench_model(64, P=48)).run(4)
+    assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-10
+
+
+def test_alpha_iteration_path(env, monkeypatch):
+    """QG_PCG_NOCERT: the fused alpha iteration (z0, alpha = (b,z0)/(z0,Bz0), psi = P(alpha z0))
+    that serves non-invertible back-projections; same answer."""
+    torch, qg, R, O = env
+    monkeypatch.setenv("QG_PCG_NOCERT", "1")
+    st = qg.run_model_no_output(qg.bench_model(64), nsteps=6, solver=1)
+    s = st.stats()
+    assert s["iters"][0] == 1 and max(s["relres"]) < 1e-13
+    ref = O.State(R.bench_model(64)).run(6)
+    assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-10
