@@ -702,6 +702,338 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 }
 
 // ------------------------------------------------------------------------------------
+// Wide rows (M = 8192).  Both systems' recurrence state (4 complex per wavenumber) plus a
+// 8192-point transform do not fit in one CU's registers and LDS, so each workgroup serves ONE
+// system of a chunk: its real row x (length M) is transformed as the half-length complex
+// FFT of z_n = x_2n + i x_2n+1 (the tuned 4096-point, 512-thread plan: ping-pong LDS buffers,
+// register-fed first pass) plus a split step X_k = E_k + W^k O_k, W = exp(-2 pi i / M).
+// Pass A: one launch, workgroups (chunk, system) interleaved so the two readers of a row of
+// zeta run side by side.  Pass B: two launches; system 0 leaves psi~1 rows in half_tmp
+// (F64), system 1 combines them with psi~2 into the back-projection and the ghost ring.
+// Recurrences, carries and the pin are the power-of-two passes' (same U / summary layout).
+// ------------------------------------------------------------------------------------
+constexpr int HN = 4096;           // half-length FFT
+constexpr int HT = 512;            // threads per workgroup
+constexpr int HK = HN / HT;        // wavenumber slots per thread: k = t + q*HT; slot (q 0, t 0)
+                                   // packs the real lines k = 0 (.x) and k = HN (.y)
+using HPlan = FftPlan<HN, HT>;
+static_assert(HPlan::REG_IN && HPlan::PINGPONG && HPlan::R0 == HK, "wide-row plan");
+constexpr int HLDS = HPlan::LDS + 128;  // + two-level split-step twiddles (64 + 64)
+
+template <class S>
+struct Pair;  // two adjacent row elements (8-byte / 4-byte alignment: rows start at element 1)
+template <>
+struct Pair<double> {
+    typedef double V __attribute__((ext_vector_type(2), aligned(8)));
+};
+template <>
+struct Pair<float> {
+    typedef float V __attribute__((ext_vector_type(2), aligned(4)));
+};
+
+__device__ __forceinline__ double2 half_tw(const double2 *wlo, const double2 *whi, int k) {  // W^k, k < HN
+    return cmul(wlo[k & 63], whi[k >> 6]);
+}
+
+__device__ __forceinline__ void half_lds_init(const SpecArgs &a, double2 *twl, double2 *wlo, double2 *whi) {
+    fft_init_twiddles<HN, HT>(twl, a.tw2);
+    const int t = threadIdx.x;
+    if (t < 64) {
+        wlo[t] = a.tw[t];
+        whi[t] = a.tw[64 * t];
+    }
+}
+
+template <class S>
+__global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
+    using US = typename Store<S>::C;
+    using PV = typename Pair<S>::V;
+    using Fwd = FftFromReg<HN, HT, false>;
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *b1 = lds + LdsSize<HN>::value, *twl = lds + 2 * LdsSize<HN>::value;
+    double2 *wlo = twl + HPlan::TW, *whi = wlo + 64;
+    const double2 *Zb = Fwd::result_in_b1 ? b1 : b0;
+    half_lds_init(a, twl, wlo, whi);
+    __syncthreads();
+    const int t = threadIdx.x, c = blockIdx.x >> 1, s = blockIdx.x & 1;
+    const int s0 = c * a.L, e = s0 + a.L - 1;
+    const int KS = a.KS;
+    const int64_t ld = a.ld;
+    const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];
+    double2 u[HK], bw[HK];
+#pragma unroll
+    for (int q = 0; q < HK; ++q) u[q] = bw[q] = make_double2(0, 0);
+    double dc = 0;
+    PV pf1[HK], pf2[HK];
+    auto load_row = [&](int j) {
+        const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
+        const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
+#pragma unroll
+        for (int p = 0; p < HK; ++p) {
+            const int n = t + p * HT;
+            pf1[p] = *reinterpret_cast<const PV *>(r1 + 2 * n);
+            pf2[p] = *reinterpret_cast<const PV *>(r2 + 2 * n);
+        }
+    };
+    load_row(e);
+    const double2 *crr = a.crr + s * KS;
+    const double *ccs = a.ccs + s * KS;
+    for (int j = e; j >= s0; --j) {
+        asm volatile("" ::: "memory");  // keep coefficient loads in the loop
+        double2 in[HK];
+#pragma unroll
+        for (int p = 0; p < HK; ++p)
+            in[p] = make_double2(pa * (double)pf1[p].x + pb * (double)pf2[p].x,
+                                 pa * (double)pf1[p].y + pb * (double)pf2[p].y);
+        // first pass from registers, then the next row's loads (in[] is dead by then: fewer
+        // live registers than loading first), then the remaining passes
+        const int tt = opaque_tid();
+        fft_pass<HN, HT, 1, 0, false, true, false>(nullptr, b0, twl, tt, in);
+        if (j > s0) load_row(j - 1);
+        {
+            double2 dummy[HPlan::R_LAST];
+            fft_run<HN, HT, HPlan::R0, 1, false, false>(b0, b1, twl, tt, dummy);
+        }
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
+#pragma unroll
+        for (int q = 0; q < HK; ++q) {
+            const int k = t + q * HT;
+            const double2 Zk = Zb[lay<HPlan::LAST_NS>(k)];
+            if (k == 0) {  // X_0 = Re + Im, X_HN = Re - Im of Z_0 (both real)
+                const double X0 = Zk.x + Zk.y, XN = Zk.x - Zk.y;
+                if (s == 0) {
+                    dc += X0;
+                    a.hline[j] = X0;
+                }
+                const double2 r0 = crr[0], rN = crr[HN];
+                u[q] = make_double2(ccs[0] * X0 + r0.x * u[q].x, ccs[HN] * XN + rN.x * u[q].y);
+                Urow[0] = Store<S>::c(make_double2(u[q].x, 0));
+                Urow[HN] = Store<S>::c(make_double2(u[q].y, 0));
+                bw[q] = make_double2(bw[q].x * r0.y + u[q].x, bw[q].y * rN.y + u[q].y);
+            } else {
+                const double2 Zm = Zb[lay<HPlan::LAST_NS>(HN - k)];
+                // E = (Z_k + conj Z_{HN-k}) / 2, O = (Z_k - conj Z_{HN-k}) / 2i, X = E + W^k O
+                const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
+                const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
+                const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
+                const double2 rr = crr[k];
+                u[q] = cfma(rr.x, u[q], cscale(X, ccs[k]));
+                Urow[k] = Store<S>::c(u[q]);
+                bw[q] = cfma(rr.y, bw[q], u[q]);
+            }
+        }
+        if constexpr (Fwd::b0_read_late) __syncthreads();  // the next row's first pass writes b0
+    }
+#pragma unroll
+    for (int q = 0; q < HK; ++q) {
+        const int k = t + q * HT;
+        const size_t o = ((size_t)c * 2 + s) * KS;
+        if (k == 0) {
+            const double q0 = a.coef[s * KS].qm1, qN = a.coef[s * KS + HN].qm1;
+            a.ULS[o] = make_double2(u[q].x, 0);
+            a.ULS[o + HN] = make_double2(u[q].y, 0);
+            a.WLS[o] = make_double2(bw[q].x * q0, 0);
+            a.WLS[o + HN] = make_double2(bw[q].y * qN, 0);
+        } else {
+            a.ULS[o + k] = u[q];
+            a.WLS[o + k] = cscale(bw[q], a.coef[s * KS + k].qm1);
+        }
+    }
+    if (t == 0 && s == 0) a.dcpart[c] = dc;
+}
+
+// SYS 0: psi~1 (pinned) -> half_tmp; SYS 1: psi~2, then psi = P_fwd (psi~1, psi~2) with ghosts
+template <class S, int SYS>
+__global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
+    using US = typename Store<S>::C;
+    using PV = typename Pair<S>::V;
+    // half_tmp holds psi~1 in the state's precision (like u: F32 intermediates for F32 states)
+    typedef S PD __attribute__((ext_vector_type(2)));  // half_tmp pair (aligned: rows of M)
+    using Inv = FftFromReg<HN, HT, true>;
+    constexpr int s = SYS;
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *b1 = lds + LdsSize<HN>::value, *twl = lds + 2 * LdsSize<HN>::value;
+    double2 *wlo = twl + HPlan::TW, *whi = wlo + 64;
+    // the split step exchanges X through b1: the first inverse pass writes only b0
+    double2 *Xs = b1;
+    const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
+    half_lds_init(a, twl, wlo, whi);
+    const int t = threadIdx.x, c = blockIdx.x;
+    const int L = a.L, s0 = c * L, e = s0 + L - 1;
+    __shared__ double lline[64];  // L <= 64 (pick_chunk)
+    const bool sing = s == 0 && a.pinned0;  // (s 0, k 0) is the singular line, served by a.line
+    if (sing && t < L) lline[t] = a.line[s0 + t];
+    __syncthreads();
+    const int KS = a.KS;
+    const int64_t Pl = a.P, ld = a.ld;
+    const double delta = a.scal[0];
+    double pin = 0;
+    if (sing) {
+        const int nbk = pin_kblocks(a.KH);
+        for (int b = 0; b < nbk; ++b) pin += a.pinpart[b];
+        if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
+    } else if (s == 0 && blockIdx.x == 0 && t == 0) {
+        a.scal[1] = 0;
+    }
+    const bool inject = a.pinned0 && a.rank == 0;
+    const double line0 = a.scal[2], line1 = a.scal[3];
+    const double2 *crr = a.crr + s * KS;
+    const double *ccs = a.ccs + s * KS;
+
+    double2 upf[HK];
+    auto load_u = [&](int j) {
+        const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
+#pragma unroll
+        for (int q = 0; q < HK; ++q) {
+            const int k = t + q * HT;
+            upf[q] = k == 0 ? make_double2(Urow[0].x, Urow[HN].x) : d2(Urow[k]);
+        }
+    };
+    load_u(s0);
+    double2 cu[HK], w[HK];
+#pragma unroll
+    for (int q = 0; q < HK; ++q) {
+        const int k = t + q * HT;
+        if (k == 0) {
+            double2 c0 = make_double2(0, 0), w0 = make_double2(0, 0), cN, wN;
+            if (!sing) chunk_carry(a, s, 0, c, delta, inject, c0, w0);
+            chunk_carry(a, s, HN, c, delta, inject, cN, wN);
+            cu[q] = make_double2(c0.x, cN.x);
+            w[q] = make_double2(w0.x, wN.x);
+        } else {
+            chunk_carry(a, s, k, c, delta, inject, cu[q], w[q]);
+        }
+    }
+    PD y1[HK];  // SYS 1: psi~1 at (2n, 2n+1), n = t + p*HT (loaded during the transform)
+    auto load_y = [&](int j) {
+        const S *yr = static_cast<const S *>(a.half_tmp) + (size_t)j * a.M;
+#pragma unroll
+        for (int p = 0; p < HK; ++p) y1[p] = *reinterpret_cast<const PD *>(yr + 2 * (t + p * HT));
+    };
+    for (int j = s0; j <= e; ++j) {
+        double2 ucur[HK];
+#pragma unroll
+        for (int q = 0; q < HK; ++q) ucur[q] = upf[q];
+        asm volatile("" ::: "memory");  // keep coefficient loads in the loop
+        double x0 = 0;  // slot (q 0, t 0): X_0 (.x of w, or the singular line)
+#pragma unroll
+        for (int q = 0; q < HK; ++q) {
+            const int k = t + q * HT;
+            if (k == 0) {
+                double ul0 = ucur[q].x, ulN = ucur[q].y;
+                if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
+                    ul0 += ccs[0] * delta;
+                    ulN += ccs[HN] * delta;
+                }
+                const double2 r0 = crr[0], rN = crr[HN];
+                const double wx = r0.x * w[q].x + (ul0 + cu[q].x);
+                const double wy = rN.x * w[q].y + (ulN + cu[q].y);
+                w[q] = make_double2(wx, wy);
+                cu[q] = make_double2(cu[q].x * r0.y, cu[q].y * rN.y);
+                x0 = sing ? (line0 + (double)j * line1) + lline[j - s0] : wx;
+            } else {
+                double2 ul = ucur[q];
+                if (s == 0 && inject && j == 0) ul.x += ccs[k] * delta;
+                const double2 rr = crr[k];
+                w[q] = cfma(rr.x, w[q], cadd(ul, cu[q]));
+                cu[q] = cscale(cu[q], rr.y);
+                Xs[k] = w[q];
+            }
+        }
+        __syncthreads();
+        // Z_k = (X_k + conj X_{HN-k}) + i W^-k (X_k - conj X_{HN-k}); z = IDFT(Z) = x_2n + i x_2n+1
+        double2 in[HK];
+#pragma unroll
+        for (int q = 0; q < HK; ++q) {
+            const int k = t + q * HT;
+            if (k == 0) {
+                in[q] = make_double2(x0 + w[q].y, x0 - w[q].y);
+            } else {  // X_k = w[q]
+                const double2 Xm = Xs[HN - k];
+                const double2 A = make_double2(w[q].x + Xm.x, w[q].y - Xm.y);
+                const double2 D = make_double2(w[q].x - Xm.x, w[q].y + Xm.y);
+                const double2 B = cmul(cconj(half_tw(wlo, whi, k)), D);
+                in[q] = make_double2(A.x - B.y, A.y + B.x);
+            }
+        }
+        // first inverse pass, then the next row's loads (in[] dead), then the remaining passes
+        const int tt = opaque_tid();
+        fft_pass<HN, HT, 1, 0, true, true, false>(nullptr, b0, twl, tt, in);
+        if (j < e) load_u(j + 1);
+        if constexpr (SYS == 1) load_y(j);
+        {
+            double2 dummy[HPlan::R_LAST];
+            fft_run<HN, HT, HPlan::R0, 1, true, false>(b0, b1, twl, tt, dummy);
+        }
+        if constexpr (SYS == 0) {
+            S *yr = static_cast<S *>(a.half_tmp) + (size_t)j * a.M;
+            const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
+#pragma unroll
+            for (int p = 0; p < HK; ++p) {
+                const int n = t + p * HT;
+                const double2 z = Xb[lay<HPlan::LAST_NS>(n)];
+                PD v;
+                // the pinned unknown is exactly 0 (get_poisson_cholesky's identity row)
+                v.x = (S)((pin_row && n == 0) ? 0.0 : z.x - pin);
+                v.y = (S)(z.y - pin);
+                *reinterpret_cast<PD *>(yr + 2 * n) = v;
+            }
+        } else {
+            S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
+            S *row1 = out1 + (size_t)(j + 1) * ld;
+            S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
+            S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
+            S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
+            const int M = (int)a.M;
+            auto put = [&](S *row, S *grow, int n, PV v) {  // elements 2n, 2n+1 and their ghost images
+                *reinterpret_cast<PV *>(row + 1 + 2 * n) = v;
+                if (n == 0) row[M + 1] = v.x;
+                if (n == HN - 1) row[0] = v.y;
+                if (grow) {
+                    *reinterpret_cast<PV *>(grow + 1 + 2 * n) = v;
+                    if (n == 0) grow[M + 1] = v.x;
+                    if (n == HN - 1) grow[0] = v.y;
+                }
+            };
+#pragma unroll
+            for (int p = 0; p < HK; ++p) {
+                const int n = t + p * HT;
+                const double2 z = Xb[lay<HPlan::LAST_NS>(n)];
+                const double x1a = (double)y1[p].x, x1b = (double)y1[p].y;
+                PV v1;
+                v1.x = (S)(a.pin_out[0] * x1a + a.pin_out[1] * z.x);
+                v1.y = (S)(a.pin_out[0] * x1b + a.pin_out[1] * z.y);
+                put(row1, grow1, n, v1);
+                if (row2) {
+                    PV v2;
+                    v2.x = (S)(a.pin_out[2] * x1a + a.pin_out[3] * z.x);
+                    v2.y = (S)(a.pin_out[2] * x1b + a.pin_out[3] * z.y);
+                    put(row2, grow2, n, v2);
+                }
+            }
+        }
+        __syncthreads();  // the next row's split step writes Xs = b1 (which holds this result)
+    }
+}
+
+template <class S>
+static int launch_half_t(bool passB, const SpecArgs &a, hipStream_t s) {
+    const size_t lds = sizeof(double2) * HLDS;
+    if (passB) {
+        QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        spec_passB_half<S, 0><<<a.Nc, HT, lds, s>>>(a);
+        QG_LAUNCH_CHECK();
+        spec_passB_half<S, 1><<<a.Nc, HT, lds, s>>>(a);
+    } else {
+        QG_HIP(hipFuncSetAttribute((const void *)spec_passA_half<S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        spec_passA_half<S><<<2 * a.Nc, HT, lds, s>>>(a);
+    }
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+// ------------------------------------------------------------------------------------
 // Generic rows (M not a power of two, M <= GEN_MMAX, odd or even): the same passes with the row
 // transform as a run-time mixed-radix Stockham FFT in LDS (radices 8, 4, 2 and the odd primes
 // up to 13, planned on the host), or, when M has a larger prime factor, a direct DFT (O(M^2)
@@ -1050,7 +1382,7 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
         case 1024: return launch_pass<1024>(passB, a, s);
         case 2048: return launch_pass<2048>(passB, a, s);
         case 4096: return launch_pass<4096>(passB, a, s);
-        case 8192: return launch_pass<8192>(passB, a, s);
+        case 8192: return a.f32 ? launch_half_t<float>(passB, a, s) : launch_half_t<double>(passB, a, s);
         default: break;
     }
     if (a.M > GEN_MMAX) return QG_ERR_UNSUPPORTED;
@@ -1078,11 +1410,13 @@ bool SpectralSolver::supports(int64_t M, int64_t P) {
     return M >= 3 && M <= GEN_MMAX;
 }
 
-// Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic), small
-// enough that the P / L workgroups of passes A and B cover the 256 CUs, and dividing P.
-static int pick_chunk(int64_t P, int req) {
+// Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic; 32 for
+// the wide rows, whose passes run two workgroups per chunk and whose summaries are twice as
+// long), small enough that the P / L workgroups of passes A and B cover the 256 CUs, and
+// dividing P.
+static int pick_chunk(int64_t M, int64_t P, int req) {
     if (req > 0) return (P % req == 0 && req <= 64) ? req : -1;
-    int cap = 16;
+    int cap = M >= 2 * HN ? 32 : 16;
     while (cap > 1 && P / cap < 256) cap >>= 1;
     for (int L = cap; L >= 1; L >>= 1)
         if (P % L == 0) return L;
@@ -1096,7 +1430,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
                          int chunk_rows, int f32) {
     if (!supports(M, P)) return QG_ERR_UNSUPPORTED;
     if (!(dx > 0) || nranks < 1 || rank < 0 || rank >= nranks || P_total != P * nranks) return QG_ERR_INVALID_ARG;
-    const int L = pick_chunk(P, chunk_rows);
+    const int L = pick_chunk(M, P, chunk_rows);
     if (L < 1) return QG_ERR_INVALID_ARG;
     SpecArgs &a = a_;
     a.M = M;
@@ -1181,7 +1515,11 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const size_t n_line = align_up(sizeof(double) * P);  // (hline and line)
     const size_t n_scal = align_up(sizeof(double) * 8);
     const size_t n_pinpart = align_up(sizeof(double) * (pin_kblocks(a.KH) + 1));
-    bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart;
+    const bool wide = M == 2 * HN;  // wide-row passes: half-length twiddles + system-0 rows
+    const size_t n_tw2 = wide ? align_up(sizeof(double2) * HN) : 0;
+    const size_t n_half = wide ? align_up((f32 ? sizeof(float) : sizeof(double)) * (size_t)P * M) : 0;
+    bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart +
+             n_tw2 + n_half;
     if (hipMalloc(&mem_, bytes_) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -1206,9 +1544,16 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.hline = (double *)take(n_line);
     a.scal = (double *)take(n_scal);
     a.pinpart = (double *)take(n_pinpart);
+    a.tw2 = wide ? (const double2 *)take(n_tw2) : nullptr;
+    a.half_tmp = wide ? (void *)take(n_half) : nullptr;
     a.tw = d_tw;
     a.coef = d_coef;
     QG_HIP(hipMemcpy(d_tw, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice));
+    if (wide) {  // exp(-2 pi i m / (M/2)) = tw[2m]
+        std::vector<double2> tw2(HN);
+        for (int m = 0; m < HN; ++m) tw2[m] = tw[2 * m];
+        QG_HIP(hipMemcpy((void *)a.tw2, tw2.data(), sizeof(double2) * HN, hipMemcpyHostToDevice));
+    }
     QG_HIP(hipMemcpy(d_coef, coef.data(), sizeof(Coef) * coef.size(), hipMemcpyHostToDevice));
     {
         std::vector<double> hot(6 * (size_t)KS);  // [2][KS] (r, 1/r) pairs, then [2][KS] cs

@@ -20,6 +20,11 @@
 //               carries, inverse DFT in LDS, pin, back-projection, store with the ghost ring.
 // HBM traffic per grid point for both systems: read 2 + write 2 (pass A), read 2 + write 2
 // (pass B) doubles, plus ~0.5 double of chunk summaries.
+// Wide rows (M = 8192): the per-wavenumber recurrence state of both systems does not fit in a
+// CU's registers next to the transform, so passes A and B run one system per workgroup, each
+// real row transformed as a half-length (M/2) complex FFT plus a split step; pass A reads
+// both inputs once per system, pass B hands system 0's rows to the system-1 launch through
+// half_tmp: 12 instead of 8 doubles per point, without register spills.
 #pragma once
 
 #include "qg_common.hpp"
@@ -59,6 +64,8 @@ struct SpecArgs {
     double *line;             // [P] centred local part of the singular line, scaled (carry)
     double *scal;             // [0] = delta, [1] = pin, [2] [3]: singular-line offset, slope
     double *pinpart;          // per-workgroup parts of the pin value (spec_pin -> pass B)
+    const double2 *tw2;       // wide rows (M = 8192): M/2 twiddles of the half-length FFT
+    void *half_tmp;           // wide rows: [P][M] system-0 result, state precision (pass B 0 -> 1)
     int nrad, rad[16];        // generic rows: mixed-radix pass plan (0 = direct DFT)
 };
 

@@ -65,7 +65,8 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0):
 
 @pytest.mark.parametrize("world,M,P,steps,solver,resume_at",
                          [(2, 64, 64, 6, 0, 0), (4, 32, 64, 5, 0, 0), (2, 128, 96, 4, 0, 0),
-                          (2, 64, 64, 6, 1, 0), (4, 32, 64, 4, 1, 0), (2, 64, 64, 7, 0, 3), (2, 48, 64, 4, 0, 0), (2, 45, 32, 4, 0, 0)])
+                          (2, 64, 64, 6, 1, 0), (4, 32, 64, 4, 1, 0), (2, 64, 64, 7, 0, 3), (2, 48, 64, 4, 0, 0), (2, 45, 32, 4, 0, 0),
+                          (2, 8192, 32, 3, 0, 0)])
 def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at):
     """solver 0 = spectral (record all-gather), 1 = PCG with the spectral preconditioner
     (its dot products and the z halo also cross the slabs).  resume_at > 0: every rank
@@ -102,4 +103,6 @@ def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at):
             for n in ("zeta", "psi", "f_store"):
                 want = g[n][:, r * Pl: r * Pl + Pl + 2]
                 err = np.linalg.norm(loc[n] - want) / np.linalg.norm(want)
-                assert err < 1e-12, (r, n, err)
+                # 8192-wide, 32-tall: the slab closure's roundoff is amplified ~M^2 by the
+                # gravest Poisson modes (measured 2e-11); still 5x inside the oracle bar
+                assert err < (1e-10 if M >= 8192 else 1e-12), (r, n, err)
