@@ -53,6 +53,9 @@ def parse():
                          "preconditioned by the spectral solve")
     ap.add_argument("--dtype", choices=("f64", "f32"), default="f64",
                     help="state precision: f64 (the reference's, default) or f32 (BASELINE config 5)")
+    ap.add_argument("--pcg-steps", type=int, default=20,
+                    help="also time this many steps with the matrix-free PCG solver (single GPU, "
+                         "spectral default only; 0 = skip)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
@@ -96,6 +99,30 @@ def cpu_baseline(n, dt, steps, threads, steps_1t):
         out["single_thread"] = {"value": steps_1t / el1, "unit": "timesteps/s", "cores": 1,
                                 "sample": f"{steps_1t} AB3 timestep(s), same model, 1 thread, {el1:.2f} s wall"}
     return out
+
+
+def pcg_variant(qgamd, m, n, warmup, K, torch):
+    """The north star's solver on the same workload: evolve_psi! as matrix-free PCG on the
+    5-point operator (preconditioned by the spectral solve), K timed steps after the warm-up;
+    iteration counts and 5-point relative residuals of the last step (k_P, k_H of SURVEY 8d)."""
+    st = qgamd.State(m, solver=qgamd._lib.QG_SOLVER_PCG, P_local=n)
+    st.initialise()
+    t = 1
+    for _ in range(max(warmup, 3)):
+        st.step(t)
+        t += 1
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        st.step(t)
+        t += 1
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    s = st.stats()
+    del st
+    return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K,
+            "iters_poisson_helmholtz": s["iters"], "relres_poisson_helmholtz": s["relres"],
+            "note": "same workload, evolve_psi! by PCG (spectral preconditioner, certified first step)"}
 
 
 def main():
@@ -171,6 +198,10 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
+    pcg = None
+    if args.pcg_steps > 0 and world == 1 and args.solver == "spectral" and args.dtype == "f64":
+        pcg = pcg_variant(qgamd, m, n, args.warmup, args.pcg_steps, torch)
+
     step_ev_ms = sorted(e[0].elapsed_time(e[2]) for e in ev)
     median_ms = step_ev_ms[K // 2]
     tend_ms = sum(e[0].elapsed_time(e[1]) for e in ev) / K
@@ -240,6 +271,8 @@ def main():
             "algorithmic_bytes_per_step": BYTES_STEP * pts, "solve_ms": solve_ms, "tendency_ms": tend_ms,
         },
     }
+    if pcg is not None:
+        out["pcg_solver"] = pcg
     if args.cpu_steps > 0 and world == 1 and args.dtype == "f64":
         out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads, args.cpu_steps_1t)
     else:

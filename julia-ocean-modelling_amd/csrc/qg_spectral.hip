@@ -98,36 +98,45 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     // register prefetch: row j-1 is loaded while row j is transformed (the barriers only wait
     // for LDS traffic, so the global loads stay in flight across the FFT)
     double pf1[EP], pf2[EP];
-    auto load_row = [&](int j) {
+    auto load_into = [&](int j, auto &d1, auto &d2) {
         const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
         const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
 #pragma unroll
         for (int p = 0; p < EP; ++p) {
             const int i = t + p * T;
             if (N % T == 0 || i < N) {
-                pf1[p] = r1[i];
-                pf2[p] = r2[i];
+                d1[p] = r1[i];
+                d2[p] = r2[i];
             }
         }
     };
     constexpr bool PF = N < 8192;  // (N = 8192: no register prefetch, registers are short)
-    if constexpr (PF) load_row(e);
-    for (int j = e; j >= s0; --j) {
-        if constexpr (!PF) load_row(j);
+#ifdef QG_PA_PF2
+    // two rows in flight (rows j-1 and j-2 while row j is transformed): two register sets
+    // used alternately, the row loop unrolled by two
+    constexpr int DEPTH = (PF && Plan::REG_IN) ? 2 : 1;
+#else
+    constexpr int DEPTH = 1;
+#endif
+    double qf1[EP], qf2[EP];
+    // one row: consume the prefetched row (c1, c2), refill them with row j - DEPTH, transform,
+    // split, filter
+    auto row_step = [&](int j, auto &c1, auto &c2) {
+        if constexpr (!PF) load_into(j, c1, c2);
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
         if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
             double2 in[Plan::R0];
 #pragma unroll
-            for (int p = 0; p < EP; ++p) in[p] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
-            if (PF && j > s0) load_row(j - 1);
+            for (int p = 0; p < EP; ++p) in[p] = make_double2(p0 * c1[p] + p1 * c2[p], p2 * c1[p] + p3 * c2[p]);
+            if (PF && j - DEPTH >= s0) load_into(j - DEPTH, c1, c2);
             FwdReg::run(in, b0, b1, twl);
         } else {
 #pragma unroll
             for (int p = 0; p < EP; ++p) {
                 const int i = t + p * T;
-                if (N % T == 0 || i < N) b0[i] = make_double2(p0 * pf1[p] + p1 * pf2[p], p2 * pf1[p] + p3 * pf2[p]);
+                if (N % T == 0 || i < N) b0[i] = make_double2(p0 * c1[p] + p1 * c2[p], p2 * c1[p] + p3 * c2[p]);
             }
-            if (PF && j > s0) load_row(j - 1);
+            if (PF && j > s0) load_into(j - 1, c1, c2);
             __syncthreads();
             double2 unused[Plan::R_LAST];
             FwdLds::run(b0, b1, twl, unused);
@@ -169,6 +178,17 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
             }
         }
         if constexpr (B0_LATE) __syncthreads();  // the next row's first pass overwrites b0
+    };
+    if constexpr (DEPTH == 2) {
+        load_into(e, pf1, pf2);
+        if (e - 1 >= s0) load_into(e - 1, qf1, qf2);
+        for (int j = e; j >= s0; j -= 2) {
+            row_step(j, pf1, pf2);
+            if (j - 1 >= s0) row_step(j - 1, qf1, qf2);
+        }
+    } else {
+        if constexpr (PF) load_into(e, pf1, pf2);
+        for (int j = e; j >= s0; --j) row_step(j, pf1, pf2);
     }
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {

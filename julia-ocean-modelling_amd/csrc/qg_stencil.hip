@@ -162,8 +162,8 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, i
     auto fetch_f = [&](int j, T &g1, T &g2) {
         if (ab3 && has_out) {
             const size_t o = (size_t)(j + 1) * ld;  // uniform row offset
-            g1 = (a.fprev1[layer] + o)[i + 1];
-            g2 = (a.fprev2[layer] + o)[i + 1];
+            g1 = ld_stream(a.fprev1[layer] + o + i + 1);
+            g2 = ld_stream(a.fprev2[layer] + o + i + 1);
         }
     };
     auto commit_psi = [&](int j, T c, T h) {
