@@ -13,6 +13,10 @@ Workload (BASELINE.json configs[2]; per GPU for N > 1, slabs in y, weak scaling)
 
 Output: one JSON line (rank 0).  `value` is whole-job throughput = (GPUs x steps) / time,
 i.e. N x N-slab timesteps per second summed over GPUs (a single GPU: model timesteps/s).
+The timed region is exactly K steps enqueued by one qg_run call; the per-kernel HIP events
+(roofline) are recorded in a second pass over the next K steps, because every event record
+adds ~5 us of queue time (A/B on one MI355X: 4096^2 1588 vs 1531 steps/s, 1024^2 11 974 vs
+10 645 with the events inside the timed loop; tools/graph_vs_stream.sh).
 """
 import argparse
 import json
@@ -56,6 +60,11 @@ def parse():
     ap.add_argument("--pcg-steps", type=int, default=20,
                     help="also time this many steps with the matrix-free PCG solver (single GPU, "
                          "spectral default only; 0 = skip)")
+    ap.add_argument("--events-in-timed", action="store_true",
+                    help="(A/B of the measurement) record the per-step HIP events inside the timed "
+                         "region instead of in a separate pass")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay the AB3 steps of qg_run as HIP graphs (QG_GRAPH=1; single GPU)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
@@ -113,9 +122,7 @@ def pcg_variant(qgamd, m, n, warmup, K, torch):
         t += 1
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(K):
-        st.step(t)
-        t += 1
+    st.run(t, K)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     s = st.stats()
@@ -127,6 +134,8 @@ def pcg_variant(qgamd, m, n, warmup, K, torch):
 
 def main():
     args = parse()
+    if args.graph:
+        os.environ["QG_GRAPH"] = "1"
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -176,13 +185,37 @@ def main():
     torch.cuda.synchronize()
 
     K = args.steps
-    stream = torch.cuda.current_stream()
-    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
+    # timed region: exactly K steps, enqueued by one qg_run call (the run_model_no_output loop,
+    # in C), bracketed by barrier + synchronize; no events inside (each HIP event record costs
+    # ~5 us of queue time on ROCm 7.2, ~2 % of a 4096^2 step, ~15 % at 1024^2)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(K)]
     t0 = time.perf_counter()
-    for k in range(K):
+    if args.events_in_timed:
+        for k in range(K):
+            ev[k][0].record(stream)
+            st.evolve_zeta_(t + k)
+            ev[k][1].record(stream)
+            st.evolve_psi_()
+            ev[k][2].record(stream)
+    else:
+        st.run(t, K)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    t += K
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    # kernel timing pass (same process, next K steps): HIP events on the library's stream
+    # around each evolve_zeta! (the tendency kernel alone on one GPU) and evolve_psi!
+    for k in range(K if not args.events_in_timed else 0):
         ev[k][0].record(stream)
         st.evolve_zeta_(t)
         ev[k][1].record(stream)
@@ -190,13 +223,6 @@ def main():
         ev[k][2].record(stream)
         t += 1
     torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
 
     pcg = None
     if args.pcg_steps > 0 and world == 1 and args.solver == "spectral" and args.dtype == "f64":
@@ -235,7 +261,7 @@ def main():
         "steps": K,
         "warmup": args.warmup,
         "ms_per_step": ms,
-        "ms_per_step_median": median_ms,
+        "ms_per_step_median_events": median_ms,
         "setup_ms": setup_ms,
         "higher_is_better": True,
         "scaling": "weak",
