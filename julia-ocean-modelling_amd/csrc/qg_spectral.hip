@@ -1,4 +1,5 @@
 // Spectral (FACR) direct solver kernels for gfx950 -- see qg_spectral.hpp for the method.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -309,6 +310,65 @@ __device__ void local_line(const SpecArgs &a, double *red, double *tile) {
     }
 }
 
+// The closure of one (system s, wavenumber k) line from the rank records: EXT = (Uext, Wext),
+// and, for the pinned system, this line's part of the pin value (returned).  Used by spec_pin
+// (after the record all-gather) and, for one rank, by spec_carry itself.
+__device__ double pin_line(const SpecArgs &a, int s, int k, double delta) {
+    const int G = a.nranks, KS = a.KS;
+    const int64_t Pl = a.P;
+    const int64_t RS = a.rec_stride;
+    auto rec = [&](int g) { return a.grec + (int64_t)g * RS; };
+    double pin_part = 0;
+    double2 *Ue = a.EXT + (size_t)s * KS + k;
+    double2 *We = a.EXT + (size_t)(2 + s) * KS + k;
+    if (s == 0 && a.pinned0 && k == 0) {
+        *Ue = make_double2(0, 0);
+        *We = make_double2(0, 0);
+        return 0;
+    }
+    const Coef cf = a.coef[s * KS + k];
+    const bool dl = (s == 0 && a.pinned0);
+    const double rPl1 = exp((double)(Pl - 1) * cf.lr);
+    auto AU = [&](int g) {
+        double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AU(KS))[s * KS + k];
+        if (dl && g == 0) v.x += cf.cs * delta;
+        return v;
+    };
+    auto AW = [&](int g) {
+        double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AW(KS))[s * KS + k];
+        if (dl && g == 0) v.x += rPl1 * (cf.cs * delta);
+        return v;
+    };
+    auto Uext = [&](int g) {  // u_true at the start of rank g+1 (ring)
+        double2 acc = make_double2(0, 0);
+        for (int m = G - 1; m >= 0; --m) acc = cfma(cf.rP, acc, AU((g + 1 + m) % G));
+        return cscale(acc, cf.inv1mrPt);
+    };
+    auto Wext = [&](int g) {  // w_true at the end of rank g-1 (ring)
+        double2 acc = make_double2(0, 0);
+        for (int m = G - 1; m >= 0; --m) {
+            const int gg = ((g - 1 - m) % G + G) % G;
+            acc = cfma(cf.rP, acc, cfma(cf.gamP, Uext(gg), AW(gg)));
+        }
+        return cscale(acc, cf.inv1mrPt);
+    };
+    const double2 ue = Uext(a.rank), we = Wext(a.rank);
+    *Ue = ue;
+    *We = we;
+    if (dl && k >= 1) {  // pinning value: rank 0, chunk 0, row 0
+        const double2 ue0 = a.rank == 0 ? ue : Uext(0);
+        const double2 we0 = a.rank == 0 ? we : Wext(0);
+        double2 u0 = reinterpret_cast<const double2 *>(rec(0) + rec_ULS0(KS))[k];
+        u0.x += cf.cs * delta;
+        const double2 uin0 = cfma(exp((double)(a.Nc - 1) * a.L * cf.lr), ue0,
+                                  reinterpret_cast<const double2 *>(rec(0) + rec_UIN0(KS))[k]);
+        const double2 w0 = cfma(cf.r, we0, cfma(cf.q, uin0, u0));
+        const double X = w0.x;
+        pin_part = (2 * k == a.M) ? X : 2 * X;
+    }
+    return pin_part;
+}
+
 // ------------------------------------------------------------------------------------
 // carry: segment-parallel chunk scans.  A workgroup owns CARRY_KB consecutive k of one
 // system; each wave's 64 lanes are CARRY_KB k x (64 / CARRY_KB) chunk segments, so the
@@ -443,6 +503,28 @@ __global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
         }
     }
     if (seg == CARRY_SEG - 1 && ok) reinterpret_cast<double2 *>(a.rec + rec_AW(KS))[s * KS + k] = w;
+    if (a.fuse_pin) {  // one rank: the closure (spec_pin's work) for this workgroup's lines
+        __shared__ double red2[CARRY_WAVES];
+        double delta = 0;
+        if (a.pinned0 && s == 0) {  // delta = -(sum of dcpart), in the extra column's order
+            double d = 0;
+            for (int cc = threadIdx.x; cc < Nc; cc += NT) d += a.dcpart[cc];
+            d = block_sum<NT>(d, red2);
+            double dd = 0;
+            dd += d;
+            delta = -dd;
+        }
+        __syncthreads();  // this workgroup's record entries (AU, AW, ULS0, UIN0) are visible
+        const double part = (seg == 0 && ok) ? pin_line(a, s, k, delta) : 0.0;
+        const double tot = block_sum<NT>(part, red2);
+        if (threadIdx.x == 0) {
+            if (s == 0) a.pinpart[blockIdx.x] = tot;
+            if (s == 0 && blockIdx.x == 0) {
+                a.scal[0] = delta;
+                if (a.pinned0) a.scal[2] = a.scal[3] = 0;  // one rank: no cross-rank line correction
+            }
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -468,55 +550,7 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
         double pin_part = 0;
         const int idx = blockIdx.x * PIN_THREADS + t;
         const int s = idx / KH, k = idx - s * KH;
-        if (idx < 2 * KH) {
-            double2 *Ue = a.EXT + (size_t)s * KS + k;
-            double2 *We = a.EXT + (size_t)(2 + s) * KS + k;
-            if (s == 0 && a.pinned0 && k == 0) {
-                *Ue = make_double2(0, 0);
-                *We = make_double2(0, 0);
-            } else {
-                const Coef cf = a.coef[s * KS + k];
-                const bool dl = (s == 0 && a.pinned0);
-                const double rPl1 = exp((double)(Pl - 1) * cf.lr);
-                auto AU = [&](int g) {
-                    double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AU(KS))[s * KS + k];
-                    if (dl && g == 0) v.x += cf.cs * delta;
-                    return v;
-                };
-                auto AW = [&](int g) {
-                    double2 v = reinterpret_cast<const double2 *>(rec(g) + rec_AW(KS))[s * KS + k];
-                    if (dl && g == 0) v.x += rPl1 * (cf.cs * delta);
-                    return v;
-                };
-                auto Uext = [&](int g) {  // u_true at the start of rank g+1 (ring)
-                    double2 acc = make_double2(0, 0);
-                    for (int m = G - 1; m >= 0; --m) acc = cfma(cf.rP, acc, AU((g + 1 + m) % G));
-                    return cscale(acc, cf.inv1mrPt);
-                };
-                auto Wext = [&](int g) {  // w_true at the end of rank g-1 (ring)
-                    double2 acc = make_double2(0, 0);
-                    for (int m = G - 1; m >= 0; --m) {
-                        const int gg = ((g - 1 - m) % G + G) % G;
-                        acc = cfma(cf.rP, acc, cfma(cf.gamP, Uext(gg), AW(gg)));
-                    }
-                    return cscale(acc, cf.inv1mrPt);
-                };
-                const double2 ue = Uext(a.rank), we = Wext(a.rank);
-                *Ue = ue;
-                *We = we;
-                if (dl && k >= 1) {  // pinning value: rank 0, chunk 0, row 0
-                    const double2 ue0 = a.rank == 0 ? ue : Uext(0);
-                    const double2 we0 = a.rank == 0 ? we : Wext(0);
-                    double2 u0 = reinterpret_cast<const double2 *>(rec(0) + rec_ULS0(KS))[k];
-                    u0.x += cf.cs * delta;
-                    const double2 uin0 = cfma(exp((double)(a.Nc - 1) * a.L * cf.lr), ue0,
-                                              reinterpret_cast<const double2 *>(rec(0) + rec_UIN0(KS))[k]);
-                    const double2 w0 = cfma(cf.r, we0, cfma(cf.q, uin0, u0));
-                    const double X = w0.x;
-                    pin_part = (2 * k == a.M) ? X : 2 * X;
-                }
-            }
-        }
+        if (idx < 2 * KH) pin_part = pin_line(a, s, k, delta);
         const double part = block_sum<PIN_THREADS>(pin_part, red);  // this workgroup's share of the pin
         if (t == 0) a.pinpart[blockIdx.x] = part;
         if (blockIdx.x == 0 && t == 0) {
@@ -543,7 +577,6 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
             }
         }
     }
-
 }
 
 // ------------------------------------------------------------------------------------
@@ -594,8 +627,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     const double delta = a.scal[0];
     double pin = 0;  // sum of the pin kernel's per-workgroup parts, fixed order
     if (a.pinned0) {
-        const int nbk = pin_kblocks(a.KH);
-        for (int b = 0; b < nbk; ++b) pin += a.pinpart[b];
+        for (int b = 0; b < a.npin; ++b) pin += a.pinpart[b];
     }
     if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     const bool inject = a.pinned0 && a.rank == 0;
@@ -889,8 +921,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     const double delta = a.scal[0];
     double pin = 0;
     if (sing) {
-        const int nbk = pin_kblocks(a.KH);
-        for (int b = 0; b < nbk; ++b) pin += a.pinpart[b];
+        for (int b = 0; b < a.npin; ++b) pin += a.pinpart[b];
         if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     } else if (s == 0 && blockIdx.x == 0 && t == 0) {
         a.scal[1] = 0;
@@ -1279,8 +1310,7 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
     const double delta = a.scal[0];
     double pin = 0;
     if (a.pinned0) {
-        const int nbk = pin_kblocks(a.KH);
-        for (int b = 0; b < nbk; ++b) pin += a.pinpart[b];
+        for (int b = 0; b < a.npin; ++b) pin += a.pinpart[b];
     }
     if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     const bool inject = a.pinned0 && a.rank == 0;
@@ -1534,7 +1564,8 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const size_t n_ext = align_up(sizeof(double2) * 4 * KS);
     const size_t n_line = align_up(sizeof(double) * P);  // (hline and line)
     const size_t n_scal = align_up(sizeof(double) * 8);
-    const size_t n_pinpart = align_up(sizeof(double) * (pin_kblocks(a.KH) + 1));
+    const int nkb = (a.KH + CARRY_KB - 1) / CARRY_KB;  // carry k-blocks (fused pin parts)
+    const size_t n_pinpart = align_up(sizeof(double) * (std::max(pin_kblocks(a.KH), nkb) + 1));
     const bool wide = M == 2 * HN;  // wide-row passes: half-length twiddles + system-0 rows
     const size_t n_tw2 = wide ? align_up(sizeof(double2) * HN) : 0;
     const size_t n_half = wide ? align_up((f32 ? sizeof(float) : sizeof(double)) * (size_t)P * M) : 0;
@@ -1607,6 +1638,9 @@ int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *ou
     a.out1 = out1;
     a.out2 = out2;
     a.write_ghost_rows = write_ghost_rows;
+    // one rank without a transport: the carry kernel closes the lines itself (no spec_pin)
+    a.fuse_pin = (a.nranks == 1 && !gather) ? 1 : 0;
+    a.npin = a.fuse_pin ? (a.KH + CARRY_KB - 1) / CARRY_KB : pin_kblocks(a.KH);
     QG_CHECK(dispatch_pass(false, a, s));
     spec_carry<<<dim3((unsigned)((a.KH + CARRY_KB - 1) / CARRY_KB) + 1, 2), 64 * CARRY_WAVES, 0, s>>>(a);
     QG_LAUNCH_CHECK();
@@ -1616,8 +1650,10 @@ int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *ou
     } else if (gather) {  // one-rank ring: still drive the transport (grec aliases rec)
         QG_CHECK(gather(user, a.rec, grec_buf_, a.rec_stride, s));
     }
-    spec_pin<<<pin_kblocks(a.KH), PIN_THREADS, 0, s>>>(a);
-    QG_LAUNCH_CHECK();
+    if (!a.fuse_pin) {
+        spec_pin<<<pin_kblocks(a.KH), PIN_THREADS, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+    }
     QG_CHECK(dispatch_pass(true, a, s));
     return QG_OK;
 }
