@@ -114,6 +114,59 @@ def test_helmholtz_manufactured_convergence(torch, qg, R):
     assert round(slope, 4) == -2.0495  # scheme_validation.ipynb
 
 
+def test_reference_cubic_laplacian_on_device(torch, qg, R):
+    """test.jl:55-69 through qg_laplace_5p: the 5-point Laplacian of x^3 + y^2 (dx = 1) is
+    exactly 6x + 2 in the interior, ghosts periodic (the reference test's `inflate` defined)."""
+    xs = np.arange(1, 11, dtype=np.float64)
+    u = R.inflate(lambda x, y: x ** 3 + y ** 2, xs, xs)
+    want = R.update_doubly_periodic_bc(R.inflate(lambda x, y: 6 * x + 2, xs, xs))
+    assert np.array_equal(host(qg.laplace_5p(dev(torch, u), 1.0)), want)
+
+
+def test_reference_arakawa_convergence_on_device(torch, qg, R):
+    """test.jl:71-103 through qg_arakawa_J: errors dx*||J - J_true|| for M = 8 .. 256 equal the
+    known values and the slope is the notebook's -2.0171."""
+    Lx = Ly = 10
+    A = lambda x, y: np.sin(2 * np.pi * x / Lx) * np.sin(2 * np.pi * y / Ly)
+    B = lambda x, y: np.cos(2 * np.pi * x / Lx) * np.cos(2 * np.pi * y / Ly)
+    TJ = lambda x, y: (-(4 * np.pi ** 2) / (Lx * Ly) * np.cos(2 * np.pi * x / Lx) ** 2
+                       * np.sin(2 * np.pi * y / Ly) ** 2
+                       + (4 * np.pi ** 2) / (Lx * Ly) * np.sin(2 * np.pi * x / Lx) ** 2
+                       * np.cos(2 * np.pi * y / Ly) ** 2)
+    Ms = [8, 16, 32, 64, 128, 256]
+    errs = []
+    for M in Ms:
+        dx = Lx / M
+        xs = R.julia_range(-dx, Lx, M + 2)
+        a, b = R.inflate(A, xs, xs), R.inflate(B, xs, xs)
+        got = host(qg.J(dx, dev(torch, a), dev(torch, b)))
+        assert np.array_equal(got, R.J(dx, a, b)), M  # bitwise the reference's J
+        errs.append(dx * np.linalg.norm(got - R.inflate(TJ, xs, xs)))
+    known = [0.84930, 0.22292, 0.054492, 0.013222, 0.0032420, 0.00080181]
+    np.testing.assert_allclose(errs, known, rtol=1e-4)
+    assert round(np.polyfit(np.log(Ms), np.log(errs), 1)[0], 4) == -2.0171
+
+
+def test_reference_poisson_convergence_window_on_device(torch, qg, R):
+    """test.jl:105-148 on the model's pinned Poisson operator through the device solver
+    (M = 4 .. 64: the generic-row and FFT passes): slope inside the reference's window."""
+    x0, x1 = 0, 3
+    Lx = x1 - x0
+    u = lambda x, y: np.sin(2 * np.pi * x / Lx) * np.cos(2 * np.pi * y / Lx)
+    f = lambda x, y: -(np.pi ** 2) * (u(x, y) * (4 / Lx ** 2 + 4 / Lx ** 2))
+    Ms = [4, 8, 16, 32, 64]
+    errs = []
+    for M in Ms:
+        dx = Lx / M
+        xs = R.julia_range(x0 - dx, x1, M + 2)
+        b = R.inflate(f, xs, xs)
+        got = host(qg.sp_solve_poisson(M, M, dx, dev(torch, b)))
+        assert rel(got, R.sp_solve_poisson(M, M, dx, b)) < 1e-12, M
+        errs.append(dx * np.linalg.norm(got - R.inflate(u, xs, xs)))
+    s = np.polyfit(np.log(Ms), np.log(errs), 1)[0]
+    assert 1.7 < -s < 2.3  # test.jl:147
+
+
 def test_initial_conditions_bitwise(torch, qg, R):
     m = qg.bench_model(32, P=24)
     st = qg.initialise_model(m)
