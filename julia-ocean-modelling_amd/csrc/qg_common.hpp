@@ -110,6 +110,19 @@ __device__ __forceinline__ T *ghost_row_target(T *out, int64_t ld, int64_t P, in
     return nullptr;
 }
 
+// XCD-aware workgroup order.  The dispatcher deals workgroups round-robin to the 8 XCDs
+// (linear id b -> XCD b % 8), each XCD with its own L2; this maps b to a logical id such that
+// each XCD receives a contiguous range of logical ids (the remainder W mod 8 keeps its id), so
+// workgroups that share data (neighbouring strips, the two systems of a wide-row chunk) share
+// an L2 and run at about the same time.
+constexpr int NUM_XCD = 8;
+__device__ __forceinline__ int xcd_logical_id() {
+    const int W = gridDim.x * gridDim.y * gridDim.z;
+    const int b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int full = W - W % NUM_XCD;
+    return b < full ? (b % NUM_XCD) * (full / NUM_XCD) + b / NUM_XCD : b;
+}
+
 // counter-based uniform in [0,1) shared with oracle/qg_ref.py and oracle/qg_oracle.c
 __host__ __device__ inline double u01(uint64_t seed, uint64_t k) {
     uint64_t x = seed + (k + 1) * 0x9E3779B97F4A7C15ULL;

@@ -759,8 +759,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 // system of a chunk: its real row x (length M) is transformed as the half-length complex
 // FFT of z_n = x_2n + i x_2n+1 (the tuned 4096-point, 512-thread plan: ping-pong LDS buffers,
 // register-fed first pass) plus a split step X_k = E_k + W^k O_k, W = exp(-2 pi i / M).
-// Pass A: one launch, workgroups (chunk, system) interleaved so the two readers of a row of
-// zeta run side by side.  Pass B: two launches; system 0 leaves psi~1 rows in half_tmp
+// Pass A: one launch, workgroups (chunk, system) adjacent in XCD-aware order so the two
+// readers of a row of zeta share an L2 and run side by side.  Pass B: two launches; system 0 leaves psi~1 rows in half_tmp
 // (F64), system 1 combines them with psi~2 into the back-projection and the ghost ring.
 // Recurrences, carries and the pin are the power-of-two passes' (same U / summary layout).
 // ------------------------------------------------------------------------------------
@@ -807,7 +807,10 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     const double2 *Zb = Fwd::result_in_b1 ? b1 : b0;
     half_lds_init(a, twl, wlo, whi);
     __syncthreads();
-    const int t = threadIdx.x, c = blockIdx.x >> 1, s = blockIdx.x & 1;
+    // the two workgroups of a chunk read the same input rows: XCD-aware order puts them on
+    // one XCD (one L2) side by side
+    const int wg = xcd_logical_id();
+    const int t = threadIdx.x, c = wg >> 1, s = wg & 1;
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
     const int64_t ld = a.ld;

@@ -86,6 +86,25 @@ __global__ void fill_ghosts_kernel(double *b, int64_t M, int64_t P, int rows_too
     }
 }
 
+// Workgroup -> (strip, row block, layer), XCD-aware: workgroups are dealt round-robin to the
+// 8 XCDs (each with its own L2), so the linear id is remapped (xcd_logical_id) to give each
+// XCD a contiguous range of logical workgroups -- whole row blocks of adjacent strips.  The
+// cache line two neighbouring strips share (rows start at element 1: strip edges are not line
+// aligned) is then fetched into one L2 instead of two: 4096^2 tendency reads 1.18 -> 1.11 GB,
+// 378 -> 364 us.  QG_TEND_NO_XCD restores the hardware order (A/B builds).
+struct TendBlock {
+    int x, y, z;
+};
+__device__ __forceinline__ TendBlock tend_block() {
+#ifdef QG_TEND_NO_XCD
+    return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
+#else
+    const int b = xcd_logical_id();
+    const int x = b % gridDim.x, r = b / gridDim.x;
+    return {x, r % (int)gridDim.y, r / (int)gridDim.y};
+#endif
+}
+
 // ------------------------------------------------------------------------------------
 // Fused tendency + Euler/AB3 update (evolve_zeta!, model.jl:155-170), one layer per
 // blockIdx.z.  Each block owns TX columns (one per thread) and marches down a strip of
@@ -98,14 +117,15 @@ __global__ void fill_ghosts_kernel(double *b, int64_t M, int64_t P, int rows_too
 template <int TX, int PF, class T>
 __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
     constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
-    const int layer = blockIdx.z;
+    const TendBlock tb = tend_block();
+    const int layer = tb.z;
     const int t = threadIdx.x;
     const int M = (int)a.M, P = (int)a.P;
     const int64_t ld = a.ld;
-    const int x0 = blockIdx.x * TX;
+    const int x0 = tb.x * TX;
     const int i = x0 + t;
     // strip rows: range A = [j0, j1) split evenly over nyA workgroups along y, then range B
-    const int y = blockIdx.y;
+    const int y = tb.y;
     const bool second = y >= nyA;
     const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
     const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
@@ -319,13 +339,14 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
     using V = typename PairT<T>::V;
     using VU = typename PairT<T>::VU;
     constexpr int RP = 6, RZ = 5, RL = 4, W = 2 * TX, WL = W + 4;
-    const int layer = blockIdx.z;
+    const TendBlock tb = tend_block();
+    const int layer = tb.z;
     const int t = threadIdx.x;
     const int M = (int)a.M, P = (int)a.P;
     const int64_t ld = a.ld;
-    const int x0 = blockIdx.x * W;
+    const int x0 = tb.x * W;
     const int xa = x0 + 2 * t;  // own points xa, xa + 1
-    const int y = blockIdx.y;
+    const int y = tb.y;
     const bool second = y >= nyA;
     const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
     const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
