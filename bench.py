@@ -45,7 +45,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=20,
+                    help="untimed steps first (the GPU clock takes ~15 steps of 4096^2 to settle)")
     ap.add_argument("--n", type=int, default=4096, help="grid points per side per GPU")
     ap.add_argument("--dt", type=float, default=60.0)
     ap.add_argument("--chunk-rows", type=int, default=0)

@@ -8,5 +8,5 @@ rc=$?; tail -3 gpurun_out/tests_$TAG.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 3
 cat gpurun_out/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o $TAG -- python3 $R/bench.py --steps 20 --warmup 5 --cpu-steps 0 --pcg-steps 0 > $R/gpurun_out/prof_$TAG.log 2>&1 || exit 4
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o $TAG -- python3 $R/bench.py --steps 50 --warmup 20 --cpu-steps 0 --pcg-steps 0 > $R/gpurun_out/prof_$TAG.log 2>&1 || exit 4
 cut -d, -f1-4 $R/gpurun_out/prof_$TAG/${TAG}_kernel_stats.csv | head -8
