@@ -49,7 +49,7 @@
 extern "C" {
 #endif
 
-#define QG_ABI_VERSION 2
+#define QG_ABI_VERSION 3
 
 typedef enum {
     QG_OK = 0,
@@ -97,6 +97,13 @@ typedef struct qg_params {
     int32_t dtype;      /* qg_dtype of the state arrays (default QG_F64; QG_F32 needs   *
                          * QG_SOLVER_SPECTRAL)                                          */
     int32_t reserved0;
+    /* Double-gyre wind forcing of the upper layer (an extension: the reference has no wind
+     * term; BASELINE config 1 names one).  With wind_tau0 != 0, zeta_f1 gains a last term
+     *   + w_j,  w_j = -(2 pi tau0 / (rho0 H_1 Ly)) sin(2 pi (j + 1/2) / P_total)
+     * for global interior row j (0-based) and Ly = P_total dx: the curl of the wind stress
+     * tau_x = -tau0 cos(2 pi y / Ly) over rho0 H_1.  Default 0 (off: the reference's RHS).  */
+    double wind_tau0;   /* N m^-2 (e.g. 0.1)                                            */
+    double wind_rho0;   /* kg m^-3 (default 1000)                                       */
 } qg_params;
 
 typedef struct qg_ctx qg_ctx;       /* one model instance (one rank) on one device       */

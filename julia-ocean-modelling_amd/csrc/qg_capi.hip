@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 #include <memory>
 #include <new>
 
@@ -69,6 +70,7 @@ struct qg_ctx {
     bool graph_ok = true;  // cleared if capture fails (then qg_run launches step by step)
     hipStream_t gstream = nullptr;
     hipEvent_t gev_in = nullptr, gev_out = nullptr;
+    double *wind = nullptr;  // [P] wind forcing of the local rows (qg_params.wind_tau0 != 0)
     double *diag = nullptr;  // diagnostics scratch: partial records | record | gathered records
     size_t diag_cap = 0;
     std::unique_ptr<SpectralSolver> spec;
@@ -115,6 +117,8 @@ void qg_default_params(qg_params *p) {
     p->pcg_rtol = 1e-12;
     p->pcg_maxit = 500;
     p->chunk_rows = 0;
+    p->wind_tau0 = 0.0;  // off: the reference's right-hand side
+    p->wind_rho0 = 1000.0;
 }
 
 static int check_params(const qg_params *p) {
@@ -124,6 +128,19 @@ static int check_params(const qg_params *p) {
     if (p->solver != QG_SOLVER_SPECTRAL && p->solver != QG_SOLVER_PCG) return QG_ERR_INVALID_ARG;
     if (p->dtype != QG_F64 && p->dtype != QG_F32) return QG_ERR_INVALID_ARG;
     if (p->dtype == QG_F32 && (p->solver != QG_SOLVER_SPECTRAL || (p->M % 2) != 0)) return QG_ERR_UNSUPPORTED;
+    if (p->wind_tau0 != 0 && !(p->wind_rho0 > 0)) return QG_ERR_INVALID_ARG;
+    return QG_OK;
+}
+
+// the wind row table of this rank's slab (built on first use; rebuilt after a comm attach)
+static int ensure_wind(qg_ctx *c) {
+    const qg_params &p = c->p;
+    if (p.wind_tau0 == 0 || c->wind) return QG_OK;
+    std::vector<double> w((size_t)p.P);
+    const int64_t Pt = p.P * c->nranks, j0 = (int64_t)c->rank * p.P;
+    for (int64_t j = 0; j < p.P; ++j) w[j] = wind_row(p.wind_tau0, p.wind_rho0, p.H_1, p.dx, Pt, j0 + j);
+    QG_HIP(hipMalloc((void **)&c->wind, sizeof(double) * p.P));
+    QG_HIP(hipMemcpy(c->wind, w.data(), sizeof(double) * p.P, hipMemcpyHostToDevice));
     return QG_OK;
 }
 
@@ -192,6 +209,7 @@ int qg_destroy(qg_ctx *c) {
     if (c->comm) comm_destroy(c->comm);
     if (c->halo) (void)hipFree(c->halo);
     if (c->diag) (void)hipFree(c->diag);
+    if (c->wind) (void)hipFree(c->wind);
     drop_graphs(c);
     if (c->gstream) (void)hipStreamDestroy(c->gstream);
     if (c->gev_in) (void)hipEventDestroy(c->gev_in);
@@ -290,6 +308,8 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     a.j0 = 0;
     a.j1 = (int)p.P;
     a.write_ghost_rows = !c->distributed;
+    QG_CHECK(ensure_wind(c));
+    a.wind = c->wind;
     for (int l = 0; l < 2; ++l) {
         a.zeta[l] = c->fieldt<T>(c->zeta, l, zh);
         a.psi[l] = c->fieldt<T>(c->psi, l, ph);
@@ -597,6 +617,10 @@ int qg_comm_unique_id(char out[128]) {
 static int comm_attach(qg_ctx *c, int nranks, int rank) {
     c->rank = rank;
     c->nranks = nranks;
+    if (c->wind) {  // the slab's global rows changed
+        (void)hipFree(c->wind);
+        c->wind = nullptr;
+    }
     c->distributed = true;  // also for nranks == 1: the ring then wraps onto itself
     if (!c->halo) QG_HIP(hipMalloc((void **)&c->halo, sizeof(double) * 16 * (size_t)(c->p.M + 2)));
     return build_solver(c);

@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 
@@ -183,8 +184,16 @@ struct TendArgsT {
     T *f_out[2];
     RowSrcT<T> zeta_rows[2];
     RowSrcT<T> psi_rows[2];
+    const double *wind;        // [P] upper-layer wind forcing per local row, or nullptr (off)
 };
 using TendArgs = TendArgsT<double>;
+
+// double-gyre wind forcing of local row j of a slab at global row offset j0 (qg_params)
+inline double wind_row(double tau0, double rho0, double H1, double dx, int64_t P_total, int64_t jg) {
+    const double pi2 = 6.283185307179586;
+    const double A = (pi2 * tau0) / (rho0 * H1 * ((double)P_total * dx));
+    return -A * std::sin(pi2 * (((double)jg + 0.5) / (double)P_total));
+}
 
 int launch_tendency(const TendArgsT<double> &a, hipStream_t s);
 int launch_tendency(const TendArgsT<float> &a, hipStream_t s);

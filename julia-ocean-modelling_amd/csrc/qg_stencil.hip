@@ -280,7 +280,8 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, i
             T last;
             if (layer == 0) last = Ut * (cdc * (Z0[cl + 1] - Z0[cl - 1]));  // U * cd(zeta)
             else last = rt * L0[cl];                                         // r * lap(psi)
-            const T F = ((v_term - J_term) - beta_term) - last;
+            T F = ((v_term - J_term) - beta_term) - last;
+            if (layer == 0 && a.wind) F = F + (T)a.wind[j];  // wind extension (off: nullptr)
             const T zcen = Z0[cl];
             const T zn = ab3 ? zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * f1c)) + ((T)(5.0 / 12.0) * f2c))
                              : zcen + (dtT * F);
@@ -512,7 +513,8 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
                 T last;
                 if (layer == 0) last = Ut * (cdc * (Zw[1][w + 1] - Zw[1][w - 1]));
                 else last = rt * L0w[w];
-                const T F = ((v_term - J_term) - beta_term) - last;
+                T F = ((v_term - J_term) - beta_term) - last;
+                if (layer == 0 && a.wind) F = F + (T)a.wind[j];  // wind extension (off: nullptr)
                 const T zcen = Zw[1][w];
                 const T g1 = v ? f1c.y : f1c.x, g2 = v ? f2c.y : f2c.x;
                 out_z[v] = ab3 ? zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * g1)) + ((T)(5.0 / 12.0) * g2))

@@ -36,6 +36,7 @@ struct QGParams
     pcg_rtol::Float64
     pcg_maxit::Int32; chunk_rows::Int32
     dtype::Int32; reserved0::Int32
+    wind_tau0::Float64; wind_rho0::Float64   # wind-forcing extension (0 = off), ABI 3
 end
 
 struct QGStats
@@ -76,11 +77,12 @@ stream_ptr() = AMDGPU.stream().stream   # hipStream_t of the task-local stream
 """Parameters of a reference `BaroclinicModel` (model.jl:12-30) in the C struct."""
 function QGParams(model; P_local::Integer=model.P, solver=SOLVER_SPECTRAL, P_fwd=(1.0, -1.0, 1.0, 1.0),
                   precond::Integer=1, pcg_rtol=1e-12, pcg_maxit::Integer=500, chunk_rows::Integer=0,
-                  dtype::Type=Float64)
+                  dtype::Type=Float64, wind_tau0=0.0, wind_rho0=1000.0)
     QGParams(model.H_1, model.H_2, model.beta, model.Lx, model.Ly, model.dt, model.T, model.U,
              model.M, P_local, model.dx, model.visc, model.r, model.R_d, model.initial_kick,
              Tuple(Float64.(P_fwd)), Int32(solver), Int32(precond), pcg_rtol, Int32(pcg_maxit),
-             Int32(chunk_rows), Int32(dtype === Float32 ? 1 : 0), Int32(0))
+             Int32(chunk_rows), Int32(dtype === Float32 ? 1 : 0), Int32(0),
+             Float64(wind_tau0), Float64(wind_rho0))
 end
 
 """

@@ -34,6 +34,7 @@ class QgParams(C.Structure):
         ("pcg_rtol", C.c_double),
         ("pcg_maxit", C.c_int32), ("chunk_rows", C.c_int32),
         ("dtype", C.c_int32), ("reserved0", C.c_int32),
+        ("wind_tau0", C.c_double), ("wind_rho0", C.c_double),
     ]
 
 

@@ -40,6 +40,7 @@ def save_checkpoint(state: State, path: str, timestep: int) -> None:
         "dtype": "f32" if p.dtype == _lib.QG_F32 else "f64",
         "solver": int(p.solver), "precond": int(p.precond), "pcg_rtol": float(p.pcg_rtol),
         "pcg_maxit": int(p.pcg_maxit), "chunk_rows": int(p.chunk_rows), "P_fwd": [float(x) for x in p.P_fwd],
+        "wind": [float(p.wind_tau0), float(p.wind_rho0)],
     }
     arrays = {n: getattr(state, n).permute(3, 2, 1, 0).contiguous().cpu().numpy()
               for n in ("zeta", "psi", "f_store")}
@@ -67,6 +68,8 @@ def load_checkpoint(path: str, device=None, **overrides):
           "pcg_maxit": meta["pcg_maxit"], "chunk_rows": meta["chunk_rows"], "P_fwd": meta["P_fwd"],
           "P_local": meta["P_local"], "rank": meta["rank"], "nranks": meta["nranks"],
           "dtype": torch.float32 if meta["dtype"] == "f32" else torch.float64}
+    if meta.get("wind", [0.0])[0] != 0.0:  # the wind-forcing extension was on
+        kw["wind"] = tuple(meta["wind"])
     kw.update(overrides)
     st = State(m, device=device, **kw)
     for n, a in arrays.items():

@@ -117,7 +117,10 @@ def P_inv_matrix(m):  # model.jl:90-99
 
 
 def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_local=None,
-              precond=_lib.QG_PRECOND_SPECTRAL, pcg_rtol=1e-12, pcg_maxit=500, dtype=_lib.QG_F64):
+              precond=_lib.QG_PRECOND_SPECTRAL, pcg_rtol=1e-12, pcg_maxit=500, dtype=_lib.QG_F64,
+              wind=None):
+    """wind = (tau0 [N m^-2], rho0 [kg m^-3]) switches on the double-gyre wind forcing
+    extension of the upper layer (include/qg_mi355.h; not in the reference)."""
     p = QgParams()
     _lib.lib().qg_default_params(C.byref(p))
     for n in ("H_1", "H_2", "beta", "Lx", "Ly", "dt", "T", "U", "dx", "visc", "r", "R_d",
@@ -134,6 +137,8 @@ def qg_params(m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0, P_loc
     p.pcg_maxit = int(pcg_maxit)
     p.chunk_rows = int(chunk_rows)
     p.dtype = int(dtype)
+    if wind is not None:
+        p.wind_tau0, p.wind_rho0 = float(wind[0]), float(wind[1])
     return p
 
 
@@ -180,9 +185,10 @@ class State:
 
     def __init__(self, m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0,
                  device=None, rank=0, nranks=1, P_local=None, precond=_lib.QG_PRECOND_SPECTRAL,
-                 pcg_rtol=1e-12, pcg_maxit=500, dtype=None):
+                 pcg_rtol=1e-12, pcg_maxit=500, dtype=None, wind=None):
         """dtype: torch.float64 (default, the reference's arithmetic) or torch.float32 (the
-        F32 state of BASELINE config 5; spectral solver only)."""
+        F32 state of BASELINE config 5; spectral solver only).  wind: (tau0, rho0) of the
+        wind-forcing extension, or None (the reference's right-hand side)."""
         _lib.lib()  # the HIP library first: no CPU fallback, fail before touching the device
         torch = _torch()
         self.model = m
@@ -195,7 +201,7 @@ class State:
         self.psi = device_zeros(m, self.P_local, dtype=self.dtype)
         self.f_store = device_zeros(m, self.P_local, dtype=self.dtype)
         self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local, precond, pcg_rtol, pcg_maxit,
-                                _lib.QG_F32 if self.dtype == torch.float32 else _lib.QG_F64)
+                                _lib.QG_F32 if self.dtype == torch.float32 else _lib.QG_F64, wind)
         self._ctx = C.c_void_p()
         call("qg_create", C.byref(self.params), int(self.device), _stream_ptr(), C.byref(self._ctx))
         call("qg_bind_state", self._ctx, _ptr(self.zeta), _ptr(self.psi), _ptr(self.f_store))

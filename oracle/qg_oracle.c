@@ -35,7 +35,17 @@ typedef struct {
     double H_1, H_2, beta, Lx, Ly, dt, T, U, dx, visc, r, R_d, initial_kick;
     long M, P;
     double Pfwd[4]; /* back-projection matrix, row-major [[p11,p12],[p21,p22]] */
+    /* wind-forcing extension (not in the reference; include/qg_mi355.h qg_params): 0 = off */
+    double wind_tau0, wind_rho0;
 } qgo_params;
+
+/* the extension's upper-layer forcing at global interior row jg (0-based) of P_total rows;
+ * the same expression as the device library's host table (qg_common.hpp wind_row) */
+static double wind_row(double tau0, double rho0, double H1, double dx, long P_total, long jg) {
+    const double pi2 = 6.283185307179586;
+    const double A = (pi2 * tau0) / (rho0 * H1 * ((double)P_total * dx));
+    return -A * sin(pi2 * (((double)jg + 0.5) / (double)P_total));
+}
 
 #define IDX(i, j, M2) ((size_t)(i) + (size_t)(M2) * (size_t)(j))
 
@@ -163,6 +173,12 @@ static void rhs(const qgo_params *m, int layer, const double *z, const double *p
         qgo_cd(z, x, M2, P2, m->dx);
         for (size_t q = 0; q < F; ++q)
             f[q] = ((m->visc * t2[q] - t3[q]) - bl * cdp[q]) - m->U * x[q];
+        if (m->wind_tau0 != 0) /* extension: + w_j, ghost rows take their periodic image */
+            for (long j = 0; j < P2; ++j) {
+                const long jj = (j - 1 + m->P) % m->P;
+                const double w = wind_row(m->wind_tau0, m->wind_rho0, m->H_1, m->dx, m->P, jj);
+                for (long i = 0; i < M2; ++i) f[IDX(i, j, M2)] = f[IDX(i, j, M2)] + w;
+            }
     } else {
         for (size_t q = 0; q < F; ++q)
             f[q] = ((m->visc * t2[q] - t3[q]) - bl * cdp[q]) - m->r * t1[q];

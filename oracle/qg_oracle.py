@@ -14,7 +14,8 @@ LIB = os.path.join(HERE, "libqg_oracle.so")
 class QgoParams(C.Structure):
     _fields_ = [(n, C.c_double) for n in
                 ("H_1", "H_2", "beta", "Lx", "Ly", "dt", "T", "U", "dx", "visc", "r", "R_d",
-                 "initial_kick")] + [("M", C.c_long), ("P", C.c_long), ("Pfwd", C.c_double * 4)]
+                 "initial_kick")] + [("M", C.c_long), ("P", C.c_long), ("Pfwd", C.c_double * 4),
+                                     ("wind_tau0", C.c_double), ("wind_rho0", C.c_double)]
 
 
 _lib = None
@@ -45,8 +46,9 @@ def lib():
     return _lib
 
 
-def params(m, P_fwd=None):
-    """QgoParams from an oracle.qg_ref.BaroclinicModel."""
+def params(m, P_fwd=None, wind=None):
+    """QgoParams from an oracle.qg_ref.BaroclinicModel; wind = (tau0, rho0) switches on the
+    wind-forcing extension (not in the reference)."""
     p = QgoParams()
     for n in ("H_1", "H_2", "beta", "Lx", "Ly", "dt", "T", "U", "dx", "visc", "r", "R_d",
               "initial_kick"):
@@ -58,6 +60,7 @@ def params(m, P_fwd=None):
         Pf = np.array([[1.0, -m.H_1 / m.H_1], [1.0, 1.0]])
     for k, v in enumerate(Pf.reshape(-1)):
         p.Pfwd[k] = float(v)
+    p.wind_tau0, p.wind_rho0 = (0.0, 1000.0) if wind is None else (float(wind[0]), float(wind[1]))
     return p
 
 
@@ -97,9 +100,9 @@ def solve(M, P, dx, alpha, f, pinned=False):
 class State:
     """(M+2,P+2,2,3) zeta/psi/f_store arrays, Fortran order (Julia layout)."""
 
-    def __init__(self, m, seeds=(20241008, 20241009), P_fwd=None, nthreads=0):
+    def __init__(self, m, seeds=(20241008, 20241009), P_fwd=None, nthreads=0, wind=None):
         self.m = m
-        self.p = params(m, P_fwd)
+        self.p = params(m, P_fwd, wind)
         self.seeds = seeds
         self.nthreads = nthreads
         shape = (m.M + 2, m.P + 2, 2, 3)

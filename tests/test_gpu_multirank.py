@@ -27,7 +27,7 @@ def _flat(d):
     return np.array([x for k in sorted(d) for x in np.atleast_1d(d[k])])
 
 
-def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0):
+def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0, wind=None):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
@@ -42,7 +42,7 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0):
     from qgamd.hostcomm import TorchDistTransport
 
     m = qgamd.bench_model(M, P=P)
-    st = qgamd.State(m, P_local=P // world, solver=solver)
+    st = qgamd.State(m, P_local=P // world, solver=solver, wind=wind)
     TorchDistTransport().attach(st, world, rank)
     st.initialise()
     if resume_at:
@@ -63,14 +63,15 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,M,P,steps,solver,resume_at",
-                         [(2, 64, 64, 6, 0, 0), (4, 32, 64, 5, 0, 0), (2, 128, 96, 4, 0, 0),
-                          (2, 64, 64, 6, 1, 0), (4, 32, 64, 4, 1, 0), (2, 64, 64, 7, 0, 3), (2, 48, 64, 4, 0, 0), (2, 45, 32, 4, 0, 0),
-                          (2, 8192, 32, 3, 0, 0)])
-def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at):
+@pytest.mark.parametrize("world,M,P,steps,solver,resume_at,wind",
+                         [(2, 64, 64, 6, 0, 0, None), (4, 32, 64, 5, 0, 0, None), (2, 128, 96, 4, 0, 0, None),
+                          (2, 64, 64, 6, 1, 0, None), (4, 32, 64, 4, 1, 0, None), (2, 64, 64, 7, 0, 3, None), (2, 48, 64, 4, 0, 0, None), (2, 45, 32, 4, 0, 0, None),
+                          (2, 8192, 32, 3, 0, 0, None), (2, 64, 64, 6, 0, 4, (0.1, 1000.0)), (4, 32, 64, 5, 0, 0, (0.1, 1000.0))])
+def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at, wind):
     """solver 0 = spectral (record all-gather), 1 = PCG with the spectral preconditioner
     (its dot products and the z halo also cross the slabs).  resume_at > 0: every rank
-    checkpoints its slab after that many steps and continues from the file."""
+    checkpoints its slab after that many steps and continues from the file.  wind: the
+    wind-forcing extension (each slab's rows at their global offset)."""
     import torch
     import torch.multiprocessing as mp
 
@@ -78,14 +79,14 @@ def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at):
         pytest.skip("no GPU")
     import qgamd
 
-    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps, solver=solver)
+    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps, solver=solver, wind=wind)
     torch.cuda.synchronize()
     g = {n: ref.to_numpy(n) for n in ("zeta", "psi", "f_store")}
     gd = _flat(ref.diagnostics())
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, resume_at))
+        procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, resume_at, wind))
                  for r in range(world)]
         for p in procs:
             p.start()

@@ -277,3 +277,23 @@ def test_physical_projection_option(torch, qg, O, R, solver):
     assert rel(st.to_numpy("zeta"), ref.zeta) < TOL
     default = qg.run_model_no_output(m, nsteps=30, solver=solver)
     assert rel(default.to_numpy("psi"), ref.psi) > 1e-3
+
+
+@pytest.mark.parametrize("solver", [0, 1])
+def test_wind_forcing_extension(torch, qg, O, R, solver):
+    """Double-gyre wind forcing of the upper layer (qg_params.wind_tau0: an extension named by
+    BASELINE config 1, not in the reference, so pinned to the C oracle's restatement of the
+    same term): the first step's state bit for bit (same row table, same order), 30 steps
+    < 1e-10, and the forcing changes the flow (against the unforced run)."""
+    M, P, wind = 64, 48, (0.1, 1000.0)
+    st = qg.initialise_model(qg.bench_model(M, P=P), solver=solver, wind=wind)
+    st.step(1)
+    ref = O.State(R.bench_model(M, P=P), wind=wind).run(1)
+    assert np.array_equal(st.to_numpy("zeta")[:, :, :, 0], ref.zeta[:, :, :, 0])
+    assert np.array_equal(st.to_numpy("f_store")[:, :, :, 0], ref.f_store[:, :, :, 0])
+    st.run(2, 29)
+    ref.run(29)
+    assert rel(st.to_numpy("psi"), ref.psi) < TOL
+    assert rel(st.to_numpy("zeta"), ref.zeta) < TOL
+    free = O.State(R.bench_model(M, P=P)).run(30)
+    assert rel(free.psi, ref.psi) > 1e-6

@@ -99,3 +99,21 @@ def test_initial_conditions_bitwise():
     z, p = R.initialise_model(m)
     st = O.State(m)
     assert np.array_equal(st.zeta, z) and np.array_equal(st.psi, p)
+
+
+def test_wind_forcing_extension_term():
+    """The wind-forcing extension (not in the reference; include/qg_mi355.h qg_params.wind_*):
+    after one Euler step the upper layer's tendency differs from the unforced one by
+    w_j = -(2 pi tau0 / (rho0 H_1 P dx)) sin(2 pi (j + 1/2) / P) on every interior row j
+    (ghost rows: their periodic images), and the lower layer is untouched."""
+    M, P, tau0, rho0 = 32, 24, 0.1, 1000.0
+    m = R.bench_model(M, P=P)
+    a = O.State(m).run(1)
+    b = O.State(m, wind=(tau0, rho0)).run(1)
+    d = b.f_store[:, :, 0, 0] - a.f_store[:, :, 0, 0]
+    j = (np.arange(P + 2) - 1) % P
+    w = -(2 * np.pi * tau0 / (rho0 * m.H_1 * (P * m.dx))) * np.sin(2 * np.pi * (j + 0.5) / P)
+    scale = np.abs(a.f_store[:, :, 0, 0]).max()
+    np.testing.assert_allclose(d, np.broadcast_to(w, d.shape), rtol=0, atol=1e-14 * np.abs(w).max() + 4e-16 * scale)
+    assert np.array_equal(b.f_store[:, :, 1, 0], a.f_store[:, :, 1, 0])
+    assert np.abs(w).max() > 0
