@@ -635,7 +635,8 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     // read before the first output row) then costs less than the idle tail of a second wave
     // (tile sweep, profiles/r01/tile_sweep_*.json: 2048^2 106 vs 111 us)
     const double pts = (double)a.M * (rA + rB);
-    const int waves = env_waves ? env_waves : (pts >= 3.0e6 && pts < 12.0e6 ? 1 : 2);
+    // four chip-fulls at 8192^2 and up (tools/tend_waves.sh: 1 422 -> 1 349 us; flat at 4096^2)
+    const int waves = env_waves ? env_waves : (pts >= 40.0e6 ? 4 : (pts >= 3.0e6 && pts < 12.0e6 ? 1 : 2));
     const int target = std::max(1, waves * sl / (2 * nx));  // row workgroups per column strip
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -659,8 +660,10 @@ static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
         sl = cus * (per > 0 ? per : 1);
     }
     const char *e = std::getenv("QG_TEND_WAVES");
-    const int waves = e ? std::max(1, std::atoi(e)) : 2;
     const int nx = (int)((a.M + W - 1) / W);
+    // four chip-fulls at 8192^2 and up (tools/tend_waves_f32.sh: 797 -> 766 us)
+    const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
+    const int waves = e ? std::max(1, std::atoi(e)) : (pts >= 40.0e6 ? 4 : 2);
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
     const int target = std::max(1, waves * sl / (2 * nx));
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
