@@ -60,6 +60,18 @@ __device__ __forceinline__ double2 cfma(double s, double2 x, double2 y) {  // s*
     return make_double2(s * x.x + y.x, s * x.y + y.y);
 }
 
+// coefficient loads of the power-of-two passes (QG_EXP_CONSTCOEF: timing experiment only,
+// constants instead of the per-row L1/L2 re-reads -- wrong results)
+#ifdef QG_EXP_CONSTCOEF
+#define QG_CRR(o) make_double2(0.5, 2.0)
+#define QG_CCS(o) 0.25
+#define QG_CR(o) 0.5
+#else
+#define QG_CRR(o) a.crr[o]
+#define QG_CCS(o) a.ccs[o]
+#define QG_CR(o) a.cr[o]
+#endif
+
 // ------------------------------------------------------------------------------------
 // pass A: project + row DFT + chunk-local backward filter (one workgroup per chunk)
 // ------------------------------------------------------------------------------------
@@ -83,15 +95,19 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
     const int64_t ld = a.ld;
-    // u: backward filter state.  bw: WLS scaled by r^-(e-j) (bw_j = bw_{j+1} r^-1 + u_j, so
-    // WLS = bw_s r^(L-1) needs no running weight).  Slot (0, t = 0): .x = k 0, .y = k N/2.
-    double2 u[KQ][2], bw[KQ][2];
+    // u: backward filter state.  bw: the chunk summary WLS = sum_j r^(e-j) u_j, accumulated
+    // with a running weight om = r^(e-j) (om *= r per row); cs = r csc.  So a row needs only r:
+    // one 8-byte load per line (the coefficient tables do not fit in L1 and are re-read from
+    // L2 every row: r01 measured ~18 us of pass A in those reloads with (r, 1/r) + cs).
+    // Slot (0, t = 0): .x = k 0, .y = k N/2.
+    double2 u[KQ][2], bw[KQ][2], om[KQ][2];
 #pragma unroll
     for (int q = 0; q < KQ; ++q)
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             u[q][s] = make_double2(0, 0);
             bw[q][s] = make_double2(0, 0);
+            om[q][s] = make_double2(1, 1);
         }
     const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
     double dc = 0;
@@ -156,12 +172,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int o0 = s * KS, oN = s * KS + NH;
-                        const double2 r0 = a.crr[o0], rN = a.crr[oN];
-                        u[q][s] = make_double2(a.ccs[o0] * B[s].x + r0.x * u[q][s].x,
-                                               a.ccs[oN] * B[s].y + rN.x * u[q][s].y);
+                        const double r0 = QG_CR(o0), rN = QG_CR(oN);
+                        u[q][s] = make_double2((r0 * a.csc) * B[s].x + r0 * u[q][s].x,
+                                               (rN * a.csc) * B[s].y + rN * u[q][s].y);
                         Urow[s * KS] = Store<S>::c(make_double2(u[q][s].x, 0));
                         Urow[s * KS + NH] = Store<S>::c(make_double2(u[q][s].y, 0));
-                        bw[q][s] = make_double2(bw[q][s].x * r0.y + u[q][s].x, bw[q][s].y * rN.y + u[q][s].y);
+                        bw[q][s] = make_double2(om[q][s].x * u[q][s].x + bw[q][s].x, om[q][s].y * u[q][s].y + bw[q][s].y);
+                        om[q][s] = make_double2(om[q][s].x * r0, om[q][s].y * rN);
                     }
                 } else {
                     const double2 Zm = Zb[lay<Plan::LAST_NS>(N - k)];
@@ -170,10 +187,11 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int o = s * KS + k;
-                        const double2 rr = a.crr[o];
-                        u[q][s] = cfma(rr.x, u[q][s], cscale(B[s], a.ccs[o]));
+                        const double r = QG_CR(o);  // cs = r csc
+                        u[q][s] = cfma(r, u[q][s], cscale(B[s], r * a.csc));
                         Urow[s * KS + k] = Store<S>::c(u[q][s]);
-                        bw[q][s] = cfma(rr.y, bw[q][s], u[q][s]);
+                        bw[q][s] = cfma(om[q][s].x, u[q][s], bw[q][s]);
+                        om[q][s].x *= r;
                     }
                 }
             }
@@ -199,14 +217,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
             for (int s = 0; s < 2; ++s) {
                 const size_t o = ((size_t)c * 2 + s) * KS;
                 if (k == 0) {
-                    const double q0 = a.coef[s * KS].qm1, qN = a.coef[s * KS + NH].qm1;
                     a.ULS[o] = make_double2(u[q][s].x, 0);
                     a.ULS[o + NH] = make_double2(u[q][s].y, 0);
-                    a.WLS[o] = make_double2(bw[q][s].x * q0, 0);
-                    a.WLS[o + NH] = make_double2(bw[q][s].y * qN, 0);
+                    a.WLS[o] = make_double2(bw[q][s].x, 0);
+                    a.WLS[o + NH] = make_double2(bw[q][s].y, 0);
                 } else {
                     a.ULS[o + k] = u[q][s];
-                    a.WLS[o + k] = cscale(bw[q][s], a.coef[s * KS + k].qm1);
+                    a.WLS[o + k] = bw[q][s];
                 }
             }
         }
@@ -674,6 +691,24 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             }
         }
     }
+#ifndef QG_COEF_LATE_B
+    // the recurrence coefficients (r, 1/r) of the next row, loaded after this row's transform
+    // (not live across it) so their L2 latency hides behind the stores
+    double2 crq[KQ][2];
+    auto load_coef = [&]() {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int k = t + q * T;
+                if (NH % T == 0 || k < NH) crq[q][s] = QG_CRR(s * KS + k);
+            }
+    };
+    load_coef();
+#define QG_PB_R(q, s, o) crq[q][s]
+#else
+#define QG_PB_R(q, s, o) QG_CRR(o)
+#endif
     for (int j = s0; j <= e; ++j) {
         if constexpr (!PF) load_u(j);
         double2 ucur[KQ][2];
@@ -697,10 +732,10 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                         const int o0 = s * KS, oN = s * KS + NH;
                         double ul0 = ucur[q][s].x, ulN = ucur[q][s].y;
                         if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
-                            ul0 += a.ccs[o0] * delta;
-                            ulN += a.ccs[oN] * delta;
+                            ul0 += QG_CCS(o0) * delta;
+                            ulN += QG_CCS(oN) * delta;
                         }
-                        const double2 r0 = a.crr[o0], rN = a.crr[oN];
+                        const double2 r0 = QG_PB_R(q, s, o0), rN = QG_CRR(oN);
                         const double wx = r0.x * w[q][s].x + (ul0 + cu[q][s].x);
                         const double wy = rN.x * w[q][s].y + (ulN + cu[q][s].y);
                         w[q][s] = make_double2(wx, wy);
@@ -715,8 +750,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                     for (int s = 0; s < 2; ++s) {
                         const int o = s * KS + k;
                         double2 ul = ucur[q][s];
-                        if (s == 0 && inject && j == 0) ul.x += a.ccs[o] * delta;
-                        const double2 rr = a.crr[o];
+                        if (s == 0 && inject && j == 0) ul.x += QG_CCS(o) * delta;
+                        const double2 rr = QG_PB_R(q, s, o);
                         w[q][s] = cfma(rr.x, w[q][s], cadd(ul, cu[q][s]));
                         cu[q][s] = cscale(cu[q][s], rr.y);
                         X[s] = w[q][s];
@@ -749,8 +784,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                 if (row2) store_row_with_ghosts(row2, grow2, N, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
             }
         }
+#ifndef QG_COEF_LATE_B
+        asm volatile("" ::: "memory");
+        if (j < e) load_coef();
+#endif
         if constexpr (Inv::b0_read_late) __syncthreads();  // the next row's recurrence writes b0
     }
+#undef QG_PB_R
 }
 
 // ------------------------------------------------------------------------------------
@@ -1557,7 +1597,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     // ---- device memory ---------------------------------------------------------------
     const size_t n_tw = align_up(sizeof(double2) * M);
     const size_t n_coef = align_up(sizeof(Coef) * coef.size());
-    const size_t n_hot = align_up(sizeof(double) * 6 * (size_t)KS);
+    const size_t n_hot = align_up(sizeof(double) * 8 * (size_t)KS);
     const size_t n_U = align_up(sizeof(double2) * (size_t)P * 2 * KS);
     const size_t n_S = align_up(sizeof(double2) * (size_t)a.Nc * 2 * KS);
     const size_t n_dc = align_up(sizeof(double) * a.Nc);
@@ -1610,15 +1650,19 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     }
     QG_HIP(hipMemcpy(d_coef, coef.data(), sizeof(Coef) * coef.size(), hipMemcpyHostToDevice));
     {
-        std::vector<double> hot(6 * (size_t)KS);  // [2][KS] (r, 1/r) pairs, then [2][KS] cs
+        // [2][KS] (r, 1/r) pairs, [2][KS] cs, [2][KS] r
+        std::vector<double> hot(8 * (size_t)KS);
         for (size_t i = 0; i < 2 * (size_t)KS; ++i) {
             hot[2 * i] = coef[i].r;
             hot[2 * i + 1] = coef[i].rinv;
             hot[4 * KS + i] = coef[i].cs;
+            hot[6 * KS + i] = coef[i].r;
         }
         QG_HIP(hipMemcpy(d_hot, hot.data(), sizeof(double) * hot.size(), hipMemcpyHostToDevice));
         a.crr = reinterpret_cast<const double2 *>(d_hot);
         a.ccs = d_hot + 4 * KS;
+        a.cr = d_hot + 6 * KS;
+        a.csc = -(dx * dx) / (double)M;
     }
     QG_HIP(hipMemset(a.rec, 0, n_rec));
     QG_HIP(hipMemset(a.scal, 0, n_scal));

@@ -52,6 +52,8 @@ struct SpecArgs {
     const Coef *coef;         // [2][KS]
     const double2 *crr;       // [2][KS] (r, 1/r) of coef, unit-stride for the row loops
     const double *ccs;        // [2][KS] cs of coef
+    const double *cr;         // [2][KS] r of coef: pass A's one 8-byte load per line and row
+    double csc;               // -dx^2 / M: cs = r csc (pass A forms cs on the fly)
     void *U;                  // [P][2][KS] complex (double2, or float2 for F32 states)
     double2 *ULS, *WLS;       // [Nc][2][KS]
     double2 *UIN, *WIN;       // [Nc][2][KS]
