@@ -855,9 +855,13 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     const int KS = a.KS;
     const int64_t ld = a.ld;
     const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];
-    double2 u[HK], bw[HK];
+    // bw = sum_j r^(e-j) u_j with the running weight om (see spec_passA): one r load per line
+    double2 u[HK], bw[HK], om[HK];
 #pragma unroll
-    for (int q = 0; q < HK; ++q) u[q] = bw[q] = make_double2(0, 0);
+    for (int q = 0; q < HK; ++q) {
+        u[q] = bw[q] = make_double2(0, 0);
+        om[q] = make_double2(1, 1);
+    }
     double dc = 0;
     PV pf1[HK], pf2[HK];
     auto load_row = [&](int j) {
@@ -871,8 +875,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         }
     };
     load_row(e);
-    const double2 *crr = a.crr + s * KS;
-    const double *ccs = a.ccs + s * KS;
+    const double *cr = a.cr + s * KS;
+    const double csc = a.csc;
     for (int j = e; j >= s0; --j) {
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop
         double2 in[HK];
@@ -900,21 +904,23 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                     dc += X0;
                     a.hline[j] = X0;
                 }
-                const double2 r0 = crr[0], rN = crr[HN];
-                u[q] = make_double2(ccs[0] * X0 + r0.x * u[q].x, ccs[HN] * XN + rN.x * u[q].y);
+                const double r0 = cr[0], rN = cr[HN];
+                u[q] = make_double2((r0 * csc) * X0 + r0 * u[q].x, (rN * csc) * XN + rN * u[q].y);
                 Urow[0] = Store<S>::c(make_double2(u[q].x, 0));
                 Urow[HN] = Store<S>::c(make_double2(u[q].y, 0));
-                bw[q] = make_double2(bw[q].x * r0.y + u[q].x, bw[q].y * rN.y + u[q].y);
+                bw[q] = make_double2(om[q].x * u[q].x + bw[q].x, om[q].y * u[q].y + bw[q].y);
+                om[q] = make_double2(om[q].x * r0, om[q].y * rN);
             } else {
                 const double2 Zm = Zb[lay<HPlan::LAST_NS>(HN - k)];
                 // E = (Z_k + conj Z_{HN-k}) / 2, O = (Z_k - conj Z_{HN-k}) / 2i, X = E + W^k O
                 const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                 const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
                 const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
-                const double2 rr = crr[k];
-                u[q] = cfma(rr.x, u[q], cscale(X, ccs[k]));
+                const double r = cr[k];
+                u[q] = cfma(r, u[q], cscale(X, r * csc));
                 Urow[k] = Store<S>::c(u[q]);
-                bw[q] = cfma(rr.y, bw[q], u[q]);
+                bw[q] = cfma(om[q].x, u[q], bw[q]);
+                om[q].x *= r;
             }
         }
         if constexpr (Fwd::b0_read_late) __syncthreads();  // the next row's first pass writes b0
@@ -924,14 +930,13 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         const int k = t + q * HT;
         const size_t o = ((size_t)c * 2 + s) * KS;
         if (k == 0) {
-            const double q0 = a.coef[s * KS].qm1, qN = a.coef[s * KS + HN].qm1;
             a.ULS[o] = make_double2(u[q].x, 0);
             a.ULS[o + HN] = make_double2(u[q].y, 0);
-            a.WLS[o] = make_double2(bw[q].x * q0, 0);
-            a.WLS[o + HN] = make_double2(bw[q].y * qN, 0);
+            a.WLS[o] = make_double2(bw[q].x, 0);
+            a.WLS[o + HN] = make_double2(bw[q].y, 0);
         } else {
             a.ULS[o + k] = u[q];
-            a.WLS[o + k] = cscale(bw[q], a.coef[s * KS + k].qm1);
+            a.WLS[o + k] = bw[q];
         }
     }
     if (t == 0 && s == 0) a.dcpart[c] = dc;
@@ -1004,6 +1009,17 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 #pragma unroll
         for (int p = 0; p < HK; ++p) y1[p] = *reinterpret_cast<const PD *>(yr + 2 * (t + p * HT));
     };
+    // SYS 0: (r, 1/r) of the next row, loaded after this row's stores (off the recurrence's
+    // critical path; the tables do not fit in L1), as in spec_passB.  SYS 1 holds the system-0
+    // rows in registers and would spill: it re-reads them at the recurrence (8192^2 F64:
+    // B0 280 -> 244 us; B1 423 -> 542 us with the early loads)
+    constexpr bool EARLY = SYS == 0;
+    double2 crq[HK];
+    auto load_coef = [&]() {
+#pragma unroll
+        for (int q = 0; q < HK; ++q) crq[q] = crr[t + q * HT];
+    };
+    if constexpr (EARLY) load_coef();
     for (int j = s0; j <= e; ++j) {
         double2 ucur[HK];
 #pragma unroll
@@ -1019,7 +1035,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                     ul0 += ccs[0] * delta;
                     ulN += ccs[HN] * delta;
                 }
-                const double2 r0 = crr[0], rN = crr[HN];
+                const double2 r0 = EARLY ? crq[q] : crr[0], rN = crr[HN];
                 const double wx = r0.x * w[q].x + (ul0 + cu[q].x);
                 const double wy = rN.x * w[q].y + (ulN + cu[q].y);
                 w[q] = make_double2(wx, wy);
@@ -1028,7 +1044,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
             } else {
                 double2 ul = ucur[q];
                 if (s == 0 && inject && j == 0) ul.x += ccs[k] * delta;
-                const double2 rr = crr[k];
+                const double2 rr = EARLY ? crq[q] : crr[k];
                 w[q] = cfma(rr.x, w[q], cadd(ul, cu[q]));
                 cu[q] = cscale(cu[q], rr.y);
                 Xs[k] = w[q];
@@ -1105,6 +1121,10 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                     put(row2, grow2, n, v2);
                 }
             }
+        }
+        if constexpr (EARLY) {
+            asm volatile("" ::: "memory");
+            if (j < e) load_coef();
         }
         __syncthreads();  // the next row's split step writes Xs = b1 (which holds this result)
     }
