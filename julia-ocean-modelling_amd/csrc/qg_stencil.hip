@@ -598,6 +598,82 @@ int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s) {
     return QG_OK;
 }
 
+// ------------------------------------------------------------------------------------
+// Cache-resident tendency (small grids).  When every field of the step fits in the 256 MB
+// MALL, the LDS-ring kernel above spends most of its time in the ring prologue and the
+// per-row barriers of short strips.  Here each thread computes one output point straight
+// from global memory: the 13-point psi diamond, the 3x3 zeta block and F(t-1), F(t-2), the
+// neighbours' re-reads served by L1/L2/MALL; no LDS, no barriers.  Same expressions in the
+// same order as tendency_kernel (lap at the five points, then the biharmonic), so the two
+// kernels are bit-identical.  Block: 64 x-points (one wave) x 4 rows.
+// ------------------------------------------------------------------------------------
+template <class T>
+__global__ __launch_bounds__(256) void tendency_direct_kernel(TendArgsT<T> a, int nyA, int nyB) {
+    const TendBlock tb = tend_block();
+    const int layer = tb.z;
+    const int M = (int)a.M, P = (int)a.P;
+    const int64_t ld = a.ld;
+    const int i = tb.x * 64 + (int)(threadIdx.x & 63);
+    const int w = (int)(threadIdx.x >> 6);
+    const int y = tb.y;
+    const bool second = y >= nyA;
+    const int r0 = second ? a.j2 : a.j0, r1 = second ? a.j3 : a.j1;
+    const int j = r0 + 4 * (second ? y - nyA : y) + w;
+    if (i >= M || j >= r1) return;  // no barriers below
+    const T *psi = a.psi[layer], *zeta = a.zeta[layer];
+    const RowSrcT<T> &prs = a.psi_rows[layer];
+    const RowSrcT<T> &zrs = a.zeta_rows[layer];
+    const T dx = (T)a.dx, idx = T(1) / dx, idx2 = idx * idx;
+    const T cdc = T(0.5) * idx;
+    const T den = T(12) * (dx * dx);
+    const T visc = (T)a.visc, dtT = (T)a.dt, Ut = (T)a.U, rt = (T)a.r;
+    const bool small = M < 8;
+    auto wx = [&](int x) -> int {
+        if (small) return ((x % M) + M) % M;
+        return x < 0 ? x + M : (x >= M ? x - M : x);
+    };
+    auto rowp = [&](const T *base, const RowSrcT<T> &rs, int jj) -> const T * {
+        if (jj >= 0 && jj < P) return base + fidx(1, jj + 1, ld);
+        return rs.halo[jj < 0 ? jj + 2 : (jj - P) + 2];
+    };
+    const T *pr[5], *zr[3];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) pr[d] = rowp(psi, prs, j - 2 + d);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) zr[d] = rowp(zeta, zrs, j - 1 + d);
+    const int xm2 = wx(i - 2), xm1 = wx(i - 1), xp1 = wx(i + 1), xp2 = wx(i + 2);
+    auto X = [&](int da) { return da == -2 ? xm2 : da == -1 ? xm1 : da == 0 ? i : da == 1 ? xp1 : xp2; };
+    auto S = [&](int da, int db) { return pr[db + 2][X(da)]; };
+    auto Z = [&](int da, int db) { return zr[db + 1][X(da)]; };
+    auto lap = [&](int da, int db) {  // lap_row's expression at (i + da, j + db)
+        return ((((S(da - 1, db) + S(da + 1, db)) - T(4) * S(da, db)) + S(da, db - 1)) + S(da, db + 1)) * idx2;
+    };
+    const T L0 = lap(0, 0);
+    const T biharm = ((((lap(-1, 0) + lap(1, 0)) - T(4) * L0) + lap(0, -1)) + lap(0, 1)) * idx2;
+    const T v_term = visc * biharm;
+    const T J_term = arakawa_point<T>(Z, S, den);
+    const T bl = (T)a.beta[layer];
+    const T beta_term = bl * (cdc * (S(1, 0) - S(-1, 0)));
+    T last;
+    if (layer == 0) last = Ut * (cdc * (Z(1, 0) - Z(-1, 0)));
+    else last = rt * L0;
+    T F = ((v_term - J_term) - beta_term) - last;
+    if (layer == 0 && a.wind) F = F + (T)a.wind[j];
+    const T zcen = Z(0, 0);
+    T zn;
+    if (a.ab3) {
+        const size_t o = (size_t)(j + 1) * ld + i + 1;
+        const T f1c = ld_stream(a.fprev1[layer] + o), f2c = ld_stream(a.fprev2[layer] + o);
+        zn = zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * f1c)) + ((T)(5.0 / 12.0) * f2c));
+    } else {
+        zn = zcen + (dtT * F);
+    }
+    T *zo = a.zeta_out[layer], *fo = a.f_out[layer];
+    const bool gr = a.write_ghost_rows;
+    store_row_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
+    store_row_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
+}
+
 template <int TX, int PF, class T>
 static int launch_tend_variant(const TendArgsT<T> &a, int rows, hipStream_t s) {
     const int nA = (a.j1 - a.j0 + rows - 1) / rows, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + rows - 1) / rows : 0;
@@ -710,6 +786,28 @@ static void tend_tile(int &w, int &r) {
 }
 
 template <class T>
+static int launch_tend_direct(const TendArgsT<T> &a, hipStream_t s) {
+    const int nA = (a.j1 - a.j0 + 3) / 4, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + 3) / 4 : 0;
+    dim3 grid((unsigned)((a.M + 63) / 64), (unsigned)(nA + nB), 2);
+    tendency_direct_kernel<T><<<grid, 256, 0, s>>>(a, nA, nB);
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+#ifndef QG_TEND_DIRECT_PTS
+#define QG_TEND_DIRECT_PTS 1.2e6  // up to ~1100^2 (tools/tend_direct.sh: 128^2 13.6 -> 7.4 us, 1024^2 33.2 -> 31.2; 1536^2 slower)
+#endif
+// QG_TEND_DIRECT: 1 forces the cache-resident kernel, 0 the ring kernel; unset = by size
+static int tend_direct_env() {
+    static int v = -2;
+    if (v == -2) {
+        const char *e = std::getenv("QG_TEND_DIRECT");
+        v = e ? std::atoi(e) : -1;
+    }
+    return v;
+}
+
+template <class T>
 static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
     if (a.j1 - a.j0 <= 0 && a.j3 - a.j2 <= 0) return QG_OK;
     int tw, tr;
@@ -725,8 +823,10 @@ static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
         if (tend_variant() == 0 && tw == 0 && tend_pair_enabled() && a.M % 2 == 0) return launch_tend_pair<256>(a, s);
     }  // (F64 pair kernel measured slower: 0.41-0.43 vs 0.386 ms at 4096^2 -- HBM-bound already)
     if (tend_variant() == 0 && tw == 0) {
-        // ~870^2 .. ~1750^2 points: 128-wide strips of 8 rows (tile sweep: 1024^2 35 vs 38 us)
         const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
+        const int de = tend_direct_env();
+        if (de == 1 || (de < 0 && pts < QG_TEND_DIRECT_PTS)) return launch_tend_direct(a, s);
+        // ~870^2 .. ~1750^2 points: 128-wide strips of 8 rows (tile sweep: 1024^2 35 vs 38 us)
         if (pts >= 0.75e6 && pts < 3.0e6) return launch_tend_variant<128, 1, T>(a, 8, s);
     }
     switch (tend_variant()) {
