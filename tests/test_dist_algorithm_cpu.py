@@ -1,5 +1,5 @@
 """The multi-rank FACR algorithm (per-rank pass A, all-gathered rank records, redundant
-cross-rank closure + pin, per-rank pass B) run as world_size 1, 2 and 4 gloo processes on the
+cross-rank closure + pin, per-rank pass B) run as world_size 1, 2, 4 and 8 gloo processes on the
 CPU, through tests/facr_model.py (the step-for-step numpy model of the device kernels),
 checked against the exact DFT solve of the C oracle on the global grid."""
 import os
@@ -51,7 +51,7 @@ def _worker(rank, world, port, M, P, L, outdir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,M,P,L", [(1, 32, 48, 8), (2, 32, 48, 8), (4, 16, 64, 4), (2, 64, 32, 16)])
+@pytest.mark.parametrize("world,M,P,L", [(1, 32, 48, 8), (2, 32, 48, 8), (4, 16, 64, 4), (2, 64, 32, 16), (8, 16, 64, 4)])
 def test_multirank_facr_matches_exact_solve(world, M, P, L):
     import torch.multiprocessing as mp
 

@@ -1,4 +1,4 @@
-"""Multi-rank (y-slab) path on the GPU: 2 and 4 ranks share the one GPU of the test box and
+"""Multi-rank (y-slab) path on the GPU: 2, 4 and 8 ranks share the one GPU of the test box and
 exchange halo rows and solver records through the host transport (qg_comm_init_host over
 torch.distributed/gloo; RCCL itself refuses several ranks on one device).  The slabs must
 reproduce the single-GPU run of the same global model: every slot of zeta, psi and f_store,
@@ -66,7 +66,8 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0, wind=
 @pytest.mark.parametrize("world,M,P,steps,solver,resume_at,wind",
                          [(2, 64, 64, 6, 0, 0, None), (4, 32, 64, 5, 0, 0, None), (2, 128, 96, 4, 0, 0, None),
                           (2, 64, 64, 6, 1, 0, None), (4, 32, 64, 4, 1, 0, None), (2, 64, 64, 7, 0, 3, None), (2, 48, 64, 4, 0, 0, None), (2, 45, 32, 4, 0, 0, None),
-                          (2, 8192, 32, 3, 0, 0, None), (2, 64, 64, 6, 0, 4, (0.1, 1000.0)), (4, 32, 64, 5, 0, 0, (0.1, 1000.0))])
+                          (2, 8192, 32, 3, 0, 0, None), (2, 64, 64, 6, 0, 4, (0.1, 1000.0)), (4, 32, 64, 5, 0, 0, (0.1, 1000.0)),
+                          (8, 64, 64, 4, 0, 0, None), (8, 32, 128, 3, 1, 0, None), (8, 1024, 64, 3, 0, 0, None)])
 def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at, wind):
     """solver 0 = spectral (record all-gather), 1 = PCG with the spectral preconditioner
     (its dot products and the z halo also cross the slabs).  resume_at > 0: every rank
