@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20,
                     help="untimed steps first (the GPU clock takes ~15 steps of 4096^2 to settle)")
-    ap.add_argument("--n", type=int, default=4096, help="grid points per side per GPU")
+    ap.add_argument("--n", "--grid", dest="n", type=int, default=4096, help="grid points per side per GPU")
     ap.add_argument("--dt", type=float, default=60.0)
     ap.add_argument("--chunk-rows", type=int, default=0)
     ap.add_argument("--cpu-steps", type=int, default=10, help="CPU-oracle sample steps (0 = skip)")
@@ -66,6 +66,10 @@ def parse():
                          "region instead of in a separate pass")
     ap.add_argument("--graph", action="store_true",
                     help="replay the AB3 steps of qg_run as HIP graphs (QG_GRAPH=1; single GPU)")
+    ap.add_argument("--transport", choices=("rccl", "host"), default="rccl",
+                    help="N > 1: RCCL over xGMI (default), or the host transport over gloo -- a "
+                         "rehearsal of the multi-rank bench with several ranks on one GPU (slow, "
+                         "not a measurement)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
@@ -145,12 +149,15 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
-    torch.cuda.set_device(local)
+    torch.cuda.set_device(local if args.transport == "rccl" else local % max(1, torch.cuda.device_count()))
     dist = None
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.transport == "host":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import qgamd
 
@@ -166,7 +173,10 @@ def main():
         buf = C.create_string_buffer(128)
         qgamd._lib.call("qg_comm_unique_id", buf)
         st.comm_init(1, 0, buf.raw)
-    if world > 1:
+    if world > 1 and args.transport == "host":
+        from qgamd.hostcomm import TorchDistTransport
+        TorchDistTransport().attach(st, world, rank)
+    elif world > 1:
         uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
         if rank == 0:
             import ctypes as C
@@ -210,7 +220,7 @@ def main():
     el = time.perf_counter() - t0
     t += K
     if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([el], dtype=torch.float64, device="cuda" if args.transport == "rccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
@@ -281,6 +291,7 @@ def main():
             "solver": ("spectral (x-DFT + parallel cyclic tridiagonal in y, direct)" if args.solver == "spectral"
                        else "matrix-free PCG on the 5-point operator, spectral preconditioner"),
             "finite": finite,
+            "transport": (args.transport if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
         },
         "roofline": {
             "bound": "hbm",
