@@ -690,7 +690,10 @@ static int launch_tend_variant(const TendArgsT<T> &a, int rows, hipStream_t s) {
 // 38 us.)
 template <class T>
 static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
-    constexpr int TX = 256, PF = 1;
+#ifndef QG_TEND_PF
+#define QG_TEND_PF 1
+#endif
+    constexpr int TX = 256, PF = QG_TEND_PF;  // register prefetch depth (rows)
     static int slots[2] = {0, 0};  // per element type
     int &sl = slots[sizeof(T) == 4];
     if (sl == 0) {
