@@ -399,7 +399,12 @@ constexpr int CARRY_KB = QG_CARRY_KB;
 constexpr int CARRY_SEG = CARRY_WAVES * (64 / CARRY_KB);
 constexpr int CARRY_REG = 8;  // chunks per segment held in registers
 
-__global__ __launch_bounds__(64 * CARRY_WAVES) void spec_carry(SpecArgs a) {
+// MINW: waves per SIMD the registers must allow.  4 lets two workgroups share a CU, for grids
+// with more carry workgroups than CUs (M = 4096: 2 x 129 + 2 = 260 on 256 CUs left 4 of them
+// for a second round; with two per CU 26.0 -> 21.8 us despite a small spill).  Smaller M keeps
+// 1 (no spill: 1024^2 11.8 vs 13.5 us).
+template <int MINW>
+__global__ __launch_bounds__(64 * CARRY_WAVES, MINW) void spec_carry(SpecArgs a) {
     __shared__ double2 agg[CARRY_SEG][CARRY_KB];
     __shared__ double qlen_s[CARRY_SEG][CARRY_KB];
     constexpr int NT = 64 * CARRY_WAVES;
@@ -1709,7 +1714,17 @@ int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *ou
     a.fuse_pin = (a.nranks == 1 && !gather) ? 1 : 0;
     a.npin = a.fuse_pin ? (a.KH + CARRY_KB - 1) / CARRY_KB : pin_kblocks(a.KH);
     QG_CHECK(dispatch_pass(false, a, s));
-    spec_carry<<<dim3((unsigned)((a.KH + CARRY_KB - 1) / CARRY_KB) + 1, 2), 64 * CARRY_WAVES, 0, s>>>(a);
+    {
+        const unsigned nkb = (unsigned)((a.KH + CARRY_KB - 1) / CARRY_KB) + 1;
+        static int cus = 0;
+        if (cus == 0) {
+            int dev = 0;
+            QG_HIP(hipGetDevice(&dev));
+            QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        }
+        if (2 * (int)nkb > cus) spec_carry<4><<<dim3(nkb, 2), 64 * CARRY_WAVES, 0, s>>>(a);
+        else spec_carry<1><<<dim3(nkb, 2), 64 * CARRY_WAVES, 0, s>>>(a);
+    }
     QG_LAUNCH_CHECK();
     if (a.nranks > 1) {
         if (!gather) return QG_ERR_RCCL;
