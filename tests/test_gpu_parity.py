@@ -243,6 +243,36 @@ def test_config2_1024_ten_steps(torch, qg, O, R):
     assert e < TOL, e
 
 
+def test_config3_4096_against_c_oracle(torch, qg, O, R):
+    """The bench workload itself (BASELINE config 3: 4096^2 F64, dt = 60 s): 3 steps (Euler,
+    Euler, AB3) against the C oracle, psi and zeta; the tendency bit for bit at step 1."""
+    N = 4096
+    st = qg.initialise_model(qg.bench_model(N, dt=60.0))
+    st.step(1)
+    ref = O.State(R.bench_model(N, dt=60.0)).run(1)
+    assert np.array_equal(st.to_numpy("zeta")[:, :, :, 0], ref.zeta[:, :, :, 0])
+    st.run(2, 2)
+    ref.run(2)
+    for n in ("psi", "zeta"):
+        e = rel(st.to_numpy(n)[:, :, :, 0], getattr(ref, n)[:, :, :, 0])
+        assert e < TOL, (n, e)
+
+
+def test_long_run_4096_stable(torch, qg):
+    """2000 steps of the bench workload (33 model hours): finite, the domain integral of zeta
+    conserved to roundoff, psi bounded (no instability at dt = 60 s)."""
+    st = qg.initialise_model(qg.bench_model(4096, dt=60.0))
+    z0 = float(st.current("zeta", 1).double()[1:-1, 1:-1].sum())
+    p0 = float(st.current("psi", 1).abs().max())
+    st.run(1, 2000)
+    torch.cuda.synchronize()
+    psi = st.current("psi", 1)
+    assert torch.isfinite(psi).all() and torch.isfinite(st.current("zeta", 1)).all()
+    z1 = st.current("zeta", 1)[1:-1, 1:-1]
+    assert abs(float(z1.sum()) - z0) < 1e-11 * float(z1.abs().max()) * z1.numel()
+    assert float(psi.abs().max()) < 10 * p0
+
+
 def test_full_size_invariants_4096(torch, qg):
     """At the 4096^2 bench size: the step conserves sum(zeta) to roundoff (Arakawa + periodic
     operators are conservative), the Poisson mode stays pinned, nothing blows up."""
