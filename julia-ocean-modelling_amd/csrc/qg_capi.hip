@@ -157,6 +157,8 @@ static int build_solver(qg_ctx *c) {
     drop_graphs(c);
     c->spec.reset();
     c->pcg.reset();
+    // the wind table is built here (create / comm attach), never inside a captured step
+    QG_CHECK(ensure_wind(c));
     if (p.solver == QG_SOLVER_PCG) {
         auto s = std::make_unique<PcgSolver>();
         QG_CHECK(s->init(p.M, p.P, p.P * c->nranks, c->rank, c->nranks, p.dx, alpha, 1, c->d.Pinv, p.P_fwd,
