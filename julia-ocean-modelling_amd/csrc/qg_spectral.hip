@@ -604,6 +604,40 @@ __global__ __launch_bounds__(PIN_THREADS) void spec_pin(SpecArgs a) {
 // ------------------------------------------------------------------------------------
 // pass B: forward filter with carries, inverse row DFT, pin, back-projection, store
 // ------------------------------------------------------------------------------------
+// The pin value is the sum of the carry / pin kernels' per-workgroup parts (pinpart[0, npin)),
+// in an order every pass B workgroup reproduces bit for bit.  pin_part() issues this thread's
+// loads (parts t, t + T, ...; the buffer is zero-padded to PIN_PAD entries) at the top of the
+// kernel; pin_total() folds them after the chunk set-up: a butterfly within the wave (both
+// lanes of a pair form a + b == b + a, so every lane ends with the same bits), then the wave
+// sums in wave order through LDS.  (A serial loop of dependent scalar loads here cost one
+// memory round trip per eight parts in front of every workgroup's first row.)
+constexpr int PIN_PAD = 1024;  // >= the widest pass B workgroup
+
+template <int T>
+__device__ __forceinline__ double pin_part(const SpecArgs &a, int t) {
+    static_assert(T <= PIN_PAD, "pinpart padding");
+    double p = a.pinpart[t];
+    for (int b = t + T; b < a.npin; b += T) p += a.pinpart[b];
+    return p;
+}
+
+template <int T>
+__device__ __forceinline__ double pin_total(double p, double *pinw) {
+    static_assert(T % 64 == 0, "whole waves");
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) p += __shfl_xor(p, m);
+    if ((threadIdx.x & 63) == 0) pinw[threadIdx.x >> 6] = p;
+    __syncthreads();
+    double s = pinw[0];
+#pragma unroll
+    for (int w = 1; w < T / 64; ++w) s += pinw[w];
+    // the same bits in every lane: keep it in scalar registers for the rows
+    const unsigned long long u = (unsigned long long)__double_as_longlong(s);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)u);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(u >> 32));
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 // carry-in state of line (s, k) entering chunk c: cu = r^L u_in, w = w_in (see header)
 __device__ __forceinline__ void chunk_carry(const SpecArgs &a, int s, int k, int c, double delta, bool inject,
                                             double2 &cu, double2 &w) {
@@ -642,16 +676,12 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     // the chunk's values of the singular line, staged once (a global load per row would sit
     // on every row's critical path, in front of the transform's barriers)
     __shared__ double lline[64];  // L <= 64 (pick_chunk)
+    __shared__ double pinw[T / 64];
     if (a.pinned0 && t < L) lline[t] = a.line[s0 + t];
-    __syncthreads();
+    const double pinp = a.pinned0 ? pin_part<T>(a, t) : 0.0;  // (lline, twl: see pin_total)
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
     const double delta = a.scal[0];
-    double pin = 0;  // sum of the pin kernel's per-workgroup parts, fixed order
-    if (a.pinned0) {
-        for (int b = 0; b < a.npin; ++b) pin += a.pinpart[b];
-    }
-    if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     const bool inject = a.pinned0 && a.rank == 0;
     const bool sing = a.pinned0;  // (s = 0, k = 0) is the singular line, served by a.line
     const double line0 = a.scal[2], line1 = a.scal[3];
@@ -714,6 +744,11 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 #else
 #define QG_PB_R(q, s, o) QG_CRR(o)
 #endif
+    // folded after the chunk set-up, so the carries' loads are not queued behind the pin
+    // parts' (folding first: 4096^2 pass B 125.9 -> 137.9 us); its barrier also publishes
+    // lline and the twiddles
+    const double pin = pin_total<T>(pinp, pinw);
+    if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     for (int j = s0; j <= e; ++j) {
         if constexpr (!PF) load_u(j);
         double2 ucur[KQ][2];
@@ -966,19 +1001,13 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     const int t = threadIdx.x, c = blockIdx.x;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     __shared__ double lline[64];  // L <= 64 (pick_chunk)
+    __shared__ double pinw[HT / 64];
     const bool sing = s == 0 && a.pinned0;  // (s 0, k 0) is the singular line, served by a.line
     if (sing && t < L) lline[t] = a.line[s0 + t];
-    __syncthreads();
+    const double pinp = sing ? pin_part<HT>(a, t) : 0.0;  // (lline, twiddles: see pin_total)
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
     const double delta = a.scal[0];
-    double pin = 0;
-    if (sing) {
-        for (int b = 0; b < a.npin; ++b) pin += a.pinpart[b];
-        if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
-    } else if (s == 0 && blockIdx.x == 0 && t == 0) {
-        a.scal[1] = 0;
-    }
     const bool inject = a.pinned0 && a.rank == 0;
     const double line0 = a.scal[2], line1 = a.scal[3];
     const double2 *crr = a.crr + s * KS;
@@ -994,6 +1023,11 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
         }
     };
     load_u(s0);
+    // folded before the chunk set-up, whose registers are short here (the pin loads were
+    // issued first, so the first row stays in flight); its barrier also publishes lline and
+    // the LDS tables of half_lds_init
+    const double pin = pin_total<HT>(pinp, pinw);
+    if (s == 0 && blockIdx.x == 0 && t == 0) a.scal[1] = pin;  // (0 when not pinned)
     double2 cu[HK], w[HK];
 #pragma unroll
     for (int q = 0; q < HK; ++q) {
@@ -1371,16 +1405,12 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
     for (int m = t; m < M; m += T) twl[m] = a.tw[m];
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     __shared__ double lline[64];  // L <= 64 (pick_chunk)
+    __shared__ double pinw[T / 64];
     if (a.pinned0 && t < L) lline[t] = a.line[s0 + t];
-    __syncthreads();
+    const double pinp = a.pinned0 ? pin_part<T>(a, t) : 0.0;  // (lline, twl: see pin_total)
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
     const double delta = a.scal[0];
-    double pin = 0;
-    if (a.pinned0) {
-        for (int b = 0; b < a.npin; ++b) pin += a.pinpart[b];
-    }
-    if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     const bool inject = a.pinned0 && a.rank == 0;
     const bool sing = a.pinned0;
     const double line0 = a.scal[2], line1 = a.scal[3];
@@ -1405,6 +1435,9 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
             }
         }
     }
+    // (its barrier also publishes lline and the twiddle table)
+    const double pin = pin_total<T>(pinp, pinw);
+    if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     for (int j = s0; j <= e; ++j) {
         const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS;
 #pragma unroll
@@ -1633,7 +1666,8 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const size_t n_line = align_up(sizeof(double) * P);  // (hline and line)
     const size_t n_scal = align_up(sizeof(double) * 8);
     const int nkb = (a.KH + CARRY_KB - 1) / CARRY_KB;  // carry k-blocks (fused pin parts)
-    const size_t n_pinpart = align_up(sizeof(double) * (std::max(pin_kblocks(a.KH), nkb) + 1));
+    // zero-padded to PIN_PAD parts: every pass B thread loads one unconditionally (pin_part)
+    const size_t n_pinpart = align_up(sizeof(double) * (std::max({pin_kblocks(a.KH), nkb, PIN_PAD}) + 1));
     const bool wide = M == 2 * HN;  // wide-row passes: half-length twiddles + system-0 rows
     const size_t n_tw2 = wide ? align_up(sizeof(double2) * HN) : 0;
     const size_t n_half = wide ? align_up((f32 ? sizeof(float) : sizeof(double)) * (size_t)P * M) : 0;
@@ -1692,6 +1726,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     QG_HIP(hipMemset(a.rec, 0, n_rec));
     QG_HIP(hipMemset(a.scal, 0, n_scal));
     QG_HIP(hipMemset(a.line, 0, n_line));
+    QG_HIP(hipMemset(a.pinpart, 0, n_pinpart));
     return QG_OK;
 }
 
