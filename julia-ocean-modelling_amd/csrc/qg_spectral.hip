@@ -90,6 +90,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
             *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
     const double2 *Zb = RES_B1 ? b1 : b0;
     fft_init_twiddles<N, T>(twl, a.tw);
+    __shared__ double crN[2];  // r of the real line k = N/2 (see spec_passB)
+    if (threadIdx.x < 2) crN[threadIdx.x] = QG_CR(threadIdx.x * a.KS + NH);
     __syncthreads();
     const int t = threadIdx.x, c = blockIdx.x;
     const int s0 = c * a.L, e = s0 + a.L - 1;
@@ -141,6 +143,22 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     auto row_step = [&](int j, auto &c1, auto &c2) {
         if constexpr (!PF) load_into(j, c1, c2);
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
+        // this row's r, issued ahead of the next row's prefetch: loads complete in order
+        // (vmcnt), so r loaded after the prefetch would make the recurrence wait for the
+        // whole next row
+#ifndef QG_PA_COEF_LATE
+        double rq[KQ][2];
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int k = t + q * T;
+                if (NH % T == 0 || k < NH) rq[q][s] = QG_CR(s * KS + k);
+            }
+#define QG_PA_R(q, s, o) rq[q][s]
+#else
+#define QG_PA_R(q, s, o) QG_CR(o)
+#endif
         if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
             double2 in[Plan::R0];
 #pragma unroll
@@ -172,7 +190,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int o0 = s * KS, oN = s * KS + NH;
-                        const double r0 = QG_CR(o0), rN = QG_CR(oN);
+                        const double r0 = QG_PA_R(q, s, o0), rN = crN[s];
+                        (void)oN;
                         u[q][s] = make_double2((r0 * a.csc) * B[s].x + r0 * u[q][s].x,
                                                (rN * a.csc) * B[s].y + rN * u[q][s].y);
                         Urow[s * KS] = Store<S>::c(make_double2(u[q][s].x, 0));
@@ -187,7 +206,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int o = s * KS + k;
-                        const double r = QG_CR(o);  // cs = r csc
+                        const double r = QG_PA_R(q, s, o);  // cs = r csc
+                        (void)o;
                         u[q][s] = cfma(r, u[q][s], cscale(B[s], r * a.csc));
                         Urow[s * KS + k] = Store<S>::c(u[q][s]);
                         bw[q][s] = cfma(om[q][s].x, u[q][s], bw[q][s]);
@@ -198,6 +218,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         }
         if constexpr (B0_LATE) __syncthreads();  // the next row's first pass overwrites b0
     };
+#undef QG_PA_R
     if constexpr (DEPTH == 2) {
         load_into(e, pf1, pf2);
         if (e - 1 >= s0) load_into(e - 1, qf1, qf2);
@@ -677,7 +698,12 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     // on every row's critical path, in front of the transform's barriers)
     __shared__ double lline[64];  // L <= 64 (pick_chunk)
     __shared__ double pinw[T / 64];
+    // (r, 1/r) of the real line k = N/2, staged like lline: read in the row loop by the lane
+    // that owns slot (0, 0), whose global load there would wait (in-order vmcnt) for the
+    // next row's prefetch, and the whole workgroup for that wave at the next barrier
+    __shared__ double2 crN[2];
     if (a.pinned0 && t < L) lline[t] = a.line[s0 + t];
+    if (N < 4096 && t < 2) crN[t] = QG_CRR(t * a.KS + NH);
     const double pinp = a.pinned0 ? pin_part<T>(a, t) : 0.0;  // (lline, twl: see pin_total)
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
@@ -775,7 +801,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                             ul0 += QG_CCS(o0) * delta;
                             ulN += QG_CCS(oN) * delta;
                         }
-                        const double2 r0 = QG_PB_R(q, s, o0), rN = QG_CRR(oN);
+                        // (N = 4096: staged costs more spill than the wait: 130.3 vs 131.7 us)
+                        const double2 r0 = QG_PB_R(q, s, o0), rN = N < 4096 ? crN[s] : QG_CRR(oN);
                         const double wx = r0.x * w[q][s].x + (ul0 + cu[q][s].x);
                         const double wy = rN.x * w[q][s].y + (ulN + cu[q][s].y);
                         w[q][s] = make_double2(wx, wy);
@@ -1002,8 +1029,10 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     __shared__ double lline[64];  // L <= 64 (pick_chunk)
     __shared__ double pinw[HT / 64];
+    __shared__ double2 crN;  // (r, 1/r) of the line k = M/2 (see spec_passB)
     const bool sing = s == 0 && a.pinned0;  // (s 0, k 0) is the singular line, served by a.line
     if (sing && t < L) lline[t] = a.line[s0 + t];
+    if (t == 0) crN = a.crr[s * a.KS + HN];
     const double pinp = sing ? pin_part<HT>(a, t) : 0.0;  // (lline, twiddles: see pin_total)
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
@@ -1074,7 +1103,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                     ul0 += ccs[0] * delta;
                     ulN += ccs[HN] * delta;
                 }
-                const double2 r0 = EARLY ? crq[q] : crr[0], rN = crr[HN];
+                const double2 r0 = EARLY ? crq[q] : crr[0], rN = crN;
                 const double wx = r0.x * w[q].x + (ul0 + cu[q].x);
                 const double wy = rN.x * w[q].y + (ulN + cu[q].y);
                 w[q] = make_double2(wx, wy);
