@@ -240,6 +240,12 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, i
             commit_zeta(j + 2, zc[0], zh[0]);
         }
         const T f1c = f1[0], f2c = f2[0];
+#ifndef QG_TEND_LATE_F
+        // land this row's F(t-1), F(t-2) (issued last iteration) before the next row's loads
+        // go out: loads complete in order (vmcnt), and with f1c / f2c first read after the
+        // new loads the compiler waited for those too (vmcnt(0)) on every row
+        asm volatile("" : : "v"(f1c), "v"(f2c) : "memory");
+#endif
 #pragma unroll
         for (int k = 0; k + 1 < PF; ++k) {
             pc[k] = pc[k + 1];
@@ -470,6 +476,9 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
             commit(sz[ring(j + 2, RZ)], zc, zh);
         }
         const V f1c = f1, f2c = f2;
+#ifndef QG_TEND_LATE_F
+        asm volatile("" : : "v"(f1c), "v"(f2c) : "memory");  // (see tendency_kernel)
+#endif
         if (j + 1 + 2 <= jb1) {
             fetch_psi(j + 4, pc, ph);
             fetch_zeta(j + 3, zc, zh);
