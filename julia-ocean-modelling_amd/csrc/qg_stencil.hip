@@ -723,8 +723,10 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     // read before the first output row) then costs less than the idle tail of a second wave
     // (tile sweep, profiles/r01/tile_sweep_*.json: 2048^2 106 vs 111 us)
     const double pts = (double)a.M * (rA + rB);
-    // four chip-fulls at 8192^2 and up (tools/tend_waves.sh: 1 422 -> 1 349 us; flat at 4096^2)
-    const int waves = env_waves ? env_waves : (pts >= 40.0e6 ? 4 : (pts >= 3.0e6 && pts < 12.0e6 ? 1 : 2));
+    // four chip-fulls at 8192^2 and up (tools/tend_waves.sh: 1 422 -> 1 349 us), three at
+    // 4096^2 (after the F-wait fix: 356.1 -> 352.0 us, three A/B pairs, tools/tend_waves_ab.sh)
+    const int waves = env_waves ? env_waves
+                                : (pts >= 40.0e6 ? 4 : (pts >= 12.0e6 ? 3 : (pts >= 3.0e6 ? 1 : 2)));
     const int target = std::max(1, waves * sl / (2 * nx));  // row workgroups per column strip
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
