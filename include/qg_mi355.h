@@ -193,6 +193,28 @@ typedef int (*qg_sendrecv_fn)(void *user, int ns, const double *const *send, con
                               const int *recv_peer, void *stream);
 int qg_comm_init_host(qg_ctx *ctx, int nranks, int rank, qg_allgather_fn allgather, qg_sendrecv_fn sendrecv,
                       void *user);
+/* Failure handling.  With a transport attached, every host wait of the context is bounded:
+ * qg_synchronize, qg_diagnostics, qg_get_stats, qg_snapshot_wait, the PCG residual reads, and
+ * a pacing wait every QG_PACE_STEPS steps of qg_step / qg_run (which keeps the host at most
+ * 2*QG_PACE_STEPS steps ahead, so a hang is seen there rather than in a blocked launch).  The
+ * wait polls the stream together with ncclCommGetAsyncError and fails with QG_ERR_RCCL --
+ * after ncclCommAbort and one stderr line naming the rank and the call -- on an RCCL error,
+ * or when no halo exchange has completed for `seconds` (default 120; the environment variable
+ * QG_COMM_TIMEOUT, read when the transport is attached, overrides it).  A failed transport
+ * stays failed: every later call that needs it returns QG_ERR_RCCL.  (The reference is one
+ * Julia process with no failure handling; this guards the multi-GPU path only.)         */
+#define QG_PACE_STEPS 16
+int qg_comm_set_timeout(qg_ctx *ctx, double seconds);
+/* The posting schedule of one halo exchange on `rank` of a ring of `nranks` y-slabs, as the
+ * library issues it (RCCL: one ncclGroupStart/End; host transport: one sendrecv call):
+ * sends k = 0, 1 go to send_peer[k] from buffer send_buf[k], receives k = 0, 1 come from
+ * recv_peer[k] into recv_buf[k]; messages between one pair of ranks match in posting order.
+ * Buffers: QG_XBUF_TO_NEXT (the slab's top rows), QG_XBUF_TO_PREV (its bottom rows),
+ * QG_XBUF_FROM_PREV (the halo below the slab), QG_XBUF_FROM_NEXT (the halo above it).
+ * Pure host function (no device needed): lets a test check the schedule for any ring size. */
+enum { QG_XBUF_TO_NEXT = 0, QG_XBUF_TO_PREV = 1, QG_XBUF_FROM_PREV = 2, QG_XBUF_FROM_NEXT = 3 };
+int qg_comm_exchange_plan(int rank, int nranks, int send_peer[2], int send_buf[2], int recv_peer[2],
+                          int recv_buf[2]);
 
 /* ---- solver handle: the get_*_cholesky analogue --------------------------------------
  * Solves, for s = 0, 1,   A_s x_s = g_s  with A_s = construct_spA(M, P, dx, alpha[s])

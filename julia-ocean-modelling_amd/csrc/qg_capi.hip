@@ -46,6 +46,10 @@ struct qg_ctx {
     size_t esize = 8;                                     // sizeof(element)
     int heads[3] = {0, 0, 0};  // physical slot of logical slot 1 for zeta, psi, f_store
     bool initialised = false;
+    // the (rank, nranks) qg_initialise seeded the state for (-1: the contents came from the
+    // caller via qg_bind_state); a transport attached later must match it, or the slabs
+    // would hold noise drawn for the wrong global rows
+    int seeded_rank = -1, seeded_nranks = -1;
     int rank = 0, nranks = 1;
     bool distributed = false;    // a transport is attached: halo exchange + record gather path
     void *comm = nullptr;        // RCCL communicator wrapper (multi-GPU)
@@ -70,6 +74,9 @@ struct qg_ctx {
     bool graph_ok = true;  // cleared if capture fails (then qg_run launches step by step)
     hipStream_t gstream = nullptr;
     hipEvent_t gev_in = nullptr, gev_out = nullptr;
+    hipEvent_t pace_ev = nullptr;  // multi-GPU pacing (qg_step)
+    bool pace_armed = false;
+    int64_t pace_count = 0;
     double *wind = nullptr;  // [P] wind forcing of the local rows (qg_params.wind_tau0 != 0)
     double *diag = nullptr;  // diagnostics scratch: partial records | record | gathered records
     size_t diag_cap = 0;
@@ -216,6 +223,7 @@ int qg_destroy(qg_ctx *c) {
     if (c->gstream) (void)hipStreamDestroy(c->gstream);
     if (c->gev_in) (void)hipEventDestroy(c->gev_in);
     if (c->gev_out) (void)hipEventDestroy(c->gev_out);
+    if (c->pace_ev) (void)hipEventDestroy(c->pace_ev);
     delete c;
     return QG_OK;
 }
@@ -228,6 +236,7 @@ int qg_bind_state(qg_ctx *c, void *zeta, void *psi, void *f_store) {
     c->fst = f_store;
     c->heads[0] = c->heads[1] = c->heads[2] = 0;
     c->initialised = true;  // caller-provided contents are taken as the reference layout
+    c->seeded_rank = c->seeded_nranks = -1;
     return QG_OK;
 }
 
@@ -242,6 +251,8 @@ int qg_initialise(qg_ctx *c, uint64_t seed1, uint64_t seed2) {
                                       c->stream));
     c->heads[0] = c->heads[1] = c->heads[2] = 0;
     c->initialised = true;
+    c->seeded_rank = c->rank;
+    c->seeded_nranks = c->nranks;
     return QG_OK;
 }
 
@@ -278,6 +289,11 @@ static int newest_fields(qg_ctx *c, double *f[6]) {
         f[4 + l] = c->field(c->fst, l, c->heads[2]);
     }
     return 6;
+}
+
+// every host wait of a context: bounded (watchdog) once a transport is attached
+static int ctx_wait(qg_ctx *c, const char *what) {
+    return comm_wait(c->distributed ? c->comm : nullptr, c->stream, nullptr, what);
 }
 
 static int flush_ghosts(qg_ctx *c) {
@@ -382,9 +398,25 @@ int qg_evolve_psi(qg_ctx *c) {
     return c->pcg ? c->last_status : QG_OK;
 }
 
+// Multi-GPU pacing: every QG_PACE_STEPS steps, wait (bounded) for the event recorded
+// QG_PACE_STEPS steps earlier, then record a new one.  The host stays 1-2 intervals ahead of
+// the device (enough to keep the queue full), and a dead peer surfaces as QG_ERR_RCCL from
+// the watchdog instead of a host blocked inside a launch on a full queue.
+static int pace(qg_ctx *c) {
+    if (!c->distributed || ++c->pace_count % QG_PACE_STEPS != 0) return QG_OK;
+    if (!c->pace_ev) QG_HIP(hipEventCreateWithFlags(&c->pace_ev, hipEventDisableTiming));
+    if (c->pace_armed) QG_CHECK(comm_wait(c->comm, c->stream, c->pace_ev, "qg_run (pacing wait)"));
+    QG_HIP(hipEventRecord(c->pace_ev, c->stream));
+    c->pace_armed = true;
+    return QG_OK;
+}
+
 int qg_step(qg_ctx *c, int64_t timestep) {
     QG_CHECK(qg_evolve_zeta(c, timestep));
-    return qg_evolve_psi(c);
+    const int st = qg_evolve_psi(c);
+    if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
+    QG_CHECK(pace(c));
+    return st;
 }
 
 // Graph replay of AB3 steps (single GPU, spectral solver: no host round trips in a step),
@@ -496,7 +528,7 @@ int qg_get_stats(qg_ctx *c, qg_stats *out) {
     double sc[2];
     QG_HIP(hipSetDevice(c->device));
     QG_HIP(hipMemcpyAsync(sc, c->spec->args().scal, sizeof(sc), hipMemcpyDeviceToHost, c->stream));
-    QG_HIP(hipStreamSynchronize(c->stream));
+    QG_CHECK(ctx_wait(c, "qg_get_stats"));
     out->delta = sc[0];
     out->pin = sc[1];
     return QG_OK;
@@ -545,7 +577,7 @@ int qg_snapshot_wait(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     if (!c->snap_inflight) return QG_OK;
     QG_HIP(hipSetDevice(c->device));
-    QG_HIP(hipEventSynchronize(c->snap_done));
+    QG_CHECK(comm_wait(c->distributed ? c->comm : nullptr, c->snap_stream, c->snap_done, "qg_snapshot_wait"));
     c->snap_inflight = false;
     return QG_OK;
 }
@@ -561,7 +593,7 @@ int qg_diagnostics(qg_ctx *c, qg_diag *out) {
     // sized for the largest world a context can join (a ctx re-attached to a bigger ring reallocates)
     const size_t need = scratch + (size_t)NREC * c->nranks;
     if (c->diag && c->diag_cap < need) {
-        QG_HIP(hipStreamSynchronize(c->stream));
+        QG_CHECK(ctx_wait(c, "qg_diagnostics"));
         QG_HIP(hipFree(c->diag));
         c->diag = nullptr;
     }
@@ -584,16 +616,19 @@ int qg_diagnostics(qg_ctx *c, qg_diag *out) {
     std::unique_ptr<double[]> h(new (std::nothrow) double[(size_t)NREC * n]);
     if (!h) return QG_ERR_ALLOC;
     QG_HIP(hipMemcpyAsync(h.get(), src, sizeof(double) * NREC * n, hipMemcpyDeviceToHost, c->stream));
-    QG_HIP(hipStreamSynchronize(c->stream));
+    QG_CHECK(ctx_wait(c, "qg_diagnostics"));
     double v[NREC];
     std::memcpy(v, h.get(), sizeof(v));
     for (int r = 1; r < n; ++r) {  // rank order: the same sums on every rank
         const double *q = h.get() + (size_t)NREC * r;
         for (int l = 0; l < 2; ++l) {
-            v[0 + l] = std::fmax(v[0 + l], q[0 + l]);
-            v[2 + l] = std::fmin(v[2 + l], q[2 + l]);
-            v[4 + l] = std::fmax(v[4 + l], q[4 + l]);
-            v[6 + l] = std::fmin(v[6 + l], q[6 + l]);
+            // NaN-propagating, like Julia's maximum / minimum (qg_diag.hip)
+            auto nmax = [](double a, double b) { return (a != a || b != b) ? a + b : std::fmax(a, b); };
+            auto nmin = [](double a, double b) { return (a != a || b != b) ? a + b : std::fmin(a, b); };
+            v[0 + l] = nmax(v[0 + l], q[0 + l]);
+            v[2 + l] = nmin(v[2 + l], q[2 + l]);
+            v[4 + l] = nmax(v[4 + l], q[4 + l]);
+            v[6 + l] = nmin(v[6 + l], q[6 + l]);
         }
         for (int k = 8; k < NREC; ++k) v[k] += q[k];
     }
@@ -606,17 +641,26 @@ int qg_synchronize(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     QG_HIP(hipSetDevice(c->device));
     QG_CHECK(flush_ghosts(c));
-    QG_HIP(hipStreamSynchronize(c->stream));
-    return QG_OK;
+    return ctx_wait(c, "qg_synchronize");
 }
 
 // ---- multi-GPU -------------------------------------------------------------------------
+int qg_comm_set_timeout(qg_ctx *c, double seconds) {
+    if (!c || !(seconds > 0)) return QG_ERR_INVALID_ARG;
+    if (!c->comm) return QG_ERR_RCCL;
+    return comm_set_timeout(c->comm, seconds);
+}
+
 int qg_comm_unique_id(char out[128]) {
     if (!out) return QG_ERR_INVALID_ARG;
     return comm_unique_id(out);
 }
 
 static int comm_attach(qg_ctx *c, int nranks, int rank) {
+    // a state seeded by qg_initialise for another slab layout holds noise drawn for the wrong
+    // global rows: refuse instead of stepping it (re-run qg_initialise after attaching)
+    if (c->initialised && c->seeded_nranks > 0 && (c->seeded_nranks != nranks || c->seeded_rank != rank))
+        return QG_ERR_INVALID_ARG;
     c->rank = rank;
     c->nranks = nranks;
     if (c->wind) {  // the slab's global rows changed

@@ -6,8 +6,12 @@
 //     grouped with the next step's halo exchange;
 //   - the spectral solver's per-step all-gather of the rank records (a few hundred KB).
 #include <rccl/rccl.h>
+#include <sched.h>
 
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "qg_common.hpp"
 
@@ -21,6 +25,12 @@ struct Comm {
     int nranks = 1, rank = 0;
     double *stage = nullptr;  // exchange staging: [to_next | to_prev | from_prev | from_next]
     size_t stage_n = 0;
+    // watchdog: the unpack kernel of every exchange stores its sequence number into this
+    // host-mapped word, so a host wait can tell "slow" from "stuck" (no exchange completing)
+    int64_t *progress_h = nullptr, *progress_d = nullptr;
+    int64_t seq = 0;
+    double timeout_s = 120.0;
+    bool failed = false;
 };
 
 #define QG_NCCL(call)                                                                          \
@@ -40,10 +50,25 @@ int comm_unique_id(char out[128]) {
     return QG_OK;
 }
 
+static int comm_setup_watchdog(Comm *c) {
+    if (const char *e = std::getenv("QG_COMM_TIMEOUT")) {
+        const double t = std::atof(e);
+        if (t > 0) c->timeout_s = t;
+    }
+    QG_HIP(hipHostMalloc((void **)&c->progress_h, sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent));
+    *c->progress_h = 0;
+    QG_HIP(hipHostGetDevicePointer((void **)&c->progress_d, c->progress_h, 0));
+    return QG_OK;
+}
+
 int comm_init(void **comm, int nranks, int rank, const char id[128]) {
     Comm *c = new Comm();
     c->nranks = nranks;
     c->rank = rank;
+    if (comm_setup_watchdog(c) != QG_OK) {
+        delete c;
+        return QG_ERR_HIP;
+    }
     {  // nranks == 1 is allowed: the halo ring then sends to itself (exercises the path)
         ncclUniqueId uid;
         std::memcpy(&uid, id, 128);
@@ -66,6 +91,10 @@ int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sen
     c->ag = ag;
     c->sr = sr;
     c->user = user;
+    if (comm_setup_watchdog(c) != QG_OK) {
+        delete c;
+        return QG_ERR_HIP;
+    }
     *comm = c;
     return QG_OK;
 }
@@ -75,14 +104,20 @@ int comm_destroy(void *comm) {
     if (!c) return QG_OK;
     if (c->nccl) ncclCommDestroy(c->nccl);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->progress_h) (void)hipHostFree(c->progress_h);
     delete c;
     return QG_OK;
 }
 
 int comm_allgather(void *user, const double *send, double *recv, int64_t count, hipStream_t s) {
     Comm *c = static_cast<Comm *>(user);
-    if (!c) return QG_ERR_RCCL;
-    if (c->ag) return c->ag(c->user, send, recv, count, s) == 0 ? QG_OK : QG_ERR_RCCL;
+    if (!c || c->failed) return QG_ERR_RCCL;
+    if (c->ag) {
+        if (c->ag(c->user, send, recv, count, s) == 0) return QG_OK;
+        std::fprintf(stderr, "qg_mi355 rank %d/%d: host transport all-gather failed\n", c->rank, c->nranks);
+        c->failed = true;
+        return QG_ERR_RCCL;
+    }
     if (!c->nccl) return QG_ERR_RCCL;
     QG_NCCL(ncclAllGather(send, recv, (size_t)count, ncclDouble, c->nccl, s));
     return QG_OK;
@@ -97,16 +132,90 @@ struct RowCopies {
     int64_t ld;
 };
 
-__global__ void copy_rows_kernel(RowCopies rc) {
+// progress != nullptr (the unpack after a receive): one lane publishes seq to the host
+__global__ void copy_rows_kernel(RowCopies rc, int64_t *progress, int64_t seq) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int k = blockIdx.y;
     if (k < rc.n && i < rc.ld) rc.dst[k][i] = rc.src[k][i];
+    if (progress && i == 0 && k == 0)
+        __hip_atomic_store(progress, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-static int copy_rows(const RowCopies &rc, hipStream_t s) {
+static int copy_rows(const RowCopies &rc, hipStream_t s, int64_t *progress = nullptr, int64_t seq = 0) {
     if (rc.n == 0) return QG_OK;
-    copy_rows_kernel<<<dim3((unsigned)((rc.ld + 255) / 256), (unsigned)rc.n), 256, 0, s>>>(rc);
+    copy_rows_kernel<<<dim3((unsigned)((rc.ld + 255) / 256), (unsigned)rc.n), 256, 0, s>>>(rc, progress, seq);
     QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+// The exchange schedule (qg_comm_exchange_plan): [send -> next, send -> prev],
+// [recv <- prev, recv <- next].  With two ranks (prev == next) the two messages per peer
+// match in this posting order: the first message from a peer is its to_next (its top rows,
+// our halo below), the second its to_prev.
+static void exchange_plan(int rank, int G, int speer[2], int sbuf[2], int rpeer[2], int rbuf[2]) {
+    const int next = (rank + 1) % G, prev = (rank - 1 + G) % G;
+    speer[0] = next; sbuf[0] = QG_XBUF_TO_NEXT;
+    speer[1] = prev; sbuf[1] = QG_XBUF_TO_PREV;
+    rpeer[0] = prev; rbuf[0] = QG_XBUF_FROM_PREV;
+    rpeer[1] = next; rbuf[1] = QG_XBUF_FROM_NEXT;
+}
+
+// Bounded host wait (see qg_comm_set_timeout in the header): polls the event (or the whole
+// stream) with the RCCL async error; fails after `timeout_s` without a completed exchange.
+int comm_wait(void *comm, hipStream_t s, hipEvent_t ev, const char *what) {
+    Comm *c = static_cast<Comm *>(comm);
+    if (!c) {
+        QG_HIP(ev ? hipEventSynchronize(ev) : hipStreamSynchronize(s));
+        return QG_OK;
+    }
+    if (c->failed) return QG_ERR_RCCL;
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto t_prog = t0;
+    int64_t seen = c->progress_h ? __atomic_load_n(c->progress_h, __ATOMIC_RELAXED) : 0;
+    for (long spin = 0;; ++spin) {
+        const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(s);
+        if (q == hipSuccess) return QG_OK;
+        if (q != hipErrorNotReady) {
+            std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: %s\n", c->rank, c->nranks, what, hipGetErrorString(q));
+            return QG_ERR_HIP;
+        }
+        const auto now = clk::now();
+        ncclResult_t ar = ncclSuccess;
+        if (c->nccl && ncclCommGetAsyncError(c->nccl, &ar) == ncclSuccess && ar != ncclSuccess &&
+            ar != ncclInProgress) {
+            std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: RCCL async error: %s; aborting the communicator\n",
+                         c->rank, c->nranks, what, ncclGetErrorString(ar));
+            ncclCommAbort(c->nccl);
+            c->nccl = nullptr;
+            c->failed = true;
+            return QG_ERR_RCCL;
+        }
+        const int64_t p = c->progress_h ? __atomic_load_n(c->progress_h, __ATOMIC_RELAXED) : 0;
+        if (p != seen) {
+            seen = p;
+            t_prog = now;
+        }
+        const double stuck = std::chrono::duration<double>(now - t_prog).count();
+        if (stuck > c->timeout_s) {
+            std::fprintf(stderr,
+                         "qg_mi355 rank %d/%d: %s: no halo exchange completed for %.1f s (last completed: #%lld of "
+                         "%lld posted) -- a peer died or posted a different schedule; aborting the communicator\n",
+                         c->rank, c->nranks, what, stuck, (long long)p, (long long)c->seq);
+            if (c->nccl) ncclCommAbort(c->nccl);
+            c->nccl = nullptr;
+            c->failed = true;
+            return QG_ERR_RCCL;
+        }
+        if (spin < 2000) sched_yield();  // the common case: done within a few ms
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+int comm_set_timeout(void *comm, double seconds) {
+    Comm *c = static_cast<Comm *>(comm);
+    if (!c || !(seconds > 0)) return QG_ERR_INVALID_ARG;
+    c->timeout_s = seconds;
     return QG_OK;
 }
 
@@ -122,12 +231,12 @@ static int copy_rows(const RowCopies &rc, hipStream_t s) {
 int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t ld,
                   int64_t P, hipStream_t s, bool ghost_f2) {
     Comm *c = static_cast<Comm *>(comm);
-    if (!c || (!c->nccl && !c->sr)) return QG_ERR_RCCL;
+    if (!c || c->failed || (!c->nccl && !c->sr)) return QG_ERR_RCCL;
     const int rows = 2 * n2 + n1;  // rows per direction
     if (n2 < 0 || n1 < 0 || 4 * n2 + (ghost_f2 ? 2 * n2 : 0) + 2 * n1 > XMAX) return QG_ERR_INVALID_ARG;
     if (rows == 0) return QG_OK;
-    const int G = c->nranks;
-    const int next = (c->rank + 1) % G, prev = (c->rank - 1 + G) % G;
+    int speer[2], sbuf[2], rpeer[2], rbuf[2];
+    exchange_plan(c->rank, c->nranks, speer, sbuf, rpeer, rbuf);
     const size_t need = (size_t)4 * rows * ld;
     if (need > c->stage_n) {
         if (c->stage) (void)hipFree(c->stage);
@@ -136,8 +245,10 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
         QG_HIP(hipMalloc((void **)&c->stage, sizeof(double) * need));
         c->stage_n = need;
     }
-    double *to_next = c->stage, *to_prev = to_next + rows * ld;
-    double *from_prev = to_prev + rows * ld, *from_next = from_prev + rows * ld;
+    double *xbuf[4];  // indexed by QG_XBUF_*
+    for (int b = 0; b < 4; ++b) xbuf[b] = c->stage + (size_t)b * rows * ld;
+    double *to_next = xbuf[QG_XBUF_TO_NEXT], *to_prev = xbuf[QG_XBUF_TO_PREV];
+    double *from_prev = xbuf[QG_XBUF_FROM_PREV], *from_next = xbuf[QG_XBUF_FROM_NEXT];
     RowCopies pk{}, up{};
     pk.ld = up.ld = ld;
     int r = 0;
@@ -165,20 +276,21 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
     QG_CHECK(copy_rows(pk, s));
     const int64_t cnt = (int64_t)rows * ld;
     if (c->sr) {
-        const double *sp[2] = {to_next, to_prev};
-        double *rp[2] = {from_prev, from_next};
+        const double *sp[2] = {xbuf[sbuf[0]], xbuf[sbuf[1]]};
+        double *rp[2] = {xbuf[rbuf[0]], xbuf[rbuf[1]]};
         const int64_t sc[2] = {cnt, cnt}, rcnt[2] = {cnt, cnt};
-        const int speer[2] = {next, prev}, rpeer[2] = {prev, next};
-        if (c->sr(c->user, 2, sp, sc, speer, 2, rp, rcnt, rpeer, s) != 0) return QG_ERR_RCCL;
+        if (c->sr(c->user, 2, sp, sc, speer, 2, rp, rcnt, rpeer, s) != 0) {
+            std::fprintf(stderr, "qg_mi355 rank %d/%d: host transport sendrecv failed\n", c->rank, c->nranks);
+            c->failed = true;
+            return QG_ERR_RCCL;
+        }
     } else {
         QG_NCCL(ncclGroupStart());
-        QG_NCCL(ncclSend(to_next, (size_t)cnt, ncclDouble, next, c->nccl, s));
-        QG_NCCL(ncclSend(to_prev, (size_t)cnt, ncclDouble, prev, c->nccl, s));
-        QG_NCCL(ncclRecv(from_prev, (size_t)cnt, ncclDouble, prev, c->nccl, s));
-        QG_NCCL(ncclRecv(from_next, (size_t)cnt, ncclDouble, next, c->nccl, s));
+        for (int k = 0; k < 2; ++k) QG_NCCL(ncclSend(xbuf[sbuf[k]], (size_t)cnt, ncclDouble, speer[k], c->nccl, s));
+        for (int k = 0; k < 2; ++k) QG_NCCL(ncclRecv(xbuf[rbuf[k]], (size_t)cnt, ncclDouble, rpeer[k], c->nccl, s));
         QG_NCCL(ncclGroupEnd());
     }
-    return copy_rows(up, s);
+    return copy_rows(up, s, c->progress_d, ++c->seq);
 }
 
 // depth == 2: halo rows into halo_buf; depth == -1: ghost-row refresh in place
@@ -189,3 +301,11 @@ int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t
 }
 
 }  // namespace qg
+
+extern "C" int qg_comm_exchange_plan(int rank, int nranks, int send_peer[2], int send_buf[2], int recv_peer[2],
+                                     int recv_buf[2]) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !send_peer || !send_buf || !recv_peer || !recv_buf)
+        return QG_ERR_INVALID_ARG;
+    qg::exchange_plan(rank, nranks, send_peer, send_buf, recv_peer, recv_buf);
+    return QG_OK;
+}

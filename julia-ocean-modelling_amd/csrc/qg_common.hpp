@@ -31,6 +31,13 @@ namespace qg {
 
 constexpr int WAVE = 64;
 
+// Bounded host wait on a stream (ev == nullptr) or an event, for a context with a transport
+// attached (comm != nullptr; qg_comm.hip): fails with QG_ERR_RCCL on an RCCL async error or
+// when no halo exchange completes within the transport's timeout.  comm == nullptr: a plain
+// hipStreamSynchronize / hipEventSynchronize.
+int comm_wait(void *comm, hipStream_t s, hipEvent_t ev, const char *what);
+int comm_set_timeout(void *comm, double seconds);
+
 __host__ __device__ inline size_t fidx(int64_t i, int64_t j, int64_t ld) {
     return static_cast<size_t>(i) + static_cast<size_t>(ld) * static_cast<size_t>(j);
 }

@@ -21,12 +21,17 @@ enum { ZMAX = 0, ZMIN = 2, PMAX = 4, PMIN = 6, ZSUM = 8, ENS = 10, KE = 12, IFAC
 __host__ __device__ constexpr bool is_min(int k) { return (k >= ZMIN && k < ZMIN + 2) || (k >= PMIN && k < PMIN + 2); }
 __host__ __device__ constexpr bool is_max(int k) { return k < ZSUM && !is_min(k); }
 
+// NaN-propagating max / min: Julia's maximum / minimum return NaN when the matrix holds one
+// (fmax / fmin would drop it and report finite extrema for a diverged run)
+__host__ __device__ inline double nmax(double a, double b) { return (a != a || b != b) ? a + b : fmax(a, b); }
+__host__ __device__ inline double nmin(double a, double b) { return (a != a || b != b) ? a + b : fmin(a, b); }
+
 __device__ inline double wave_max(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    for (int o = 32; o > 0; o >>= 1) v = nmax(v, __shfl_xor(v, o));
     return v;
 }
 __device__ inline double wave_min(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    for (int o = 32; o > 0; o >>= 1) v = nmin(v, __shfl_xor(v, o));
     return v;
 }
 __device__ inline double wave_sum(double v) {
@@ -52,8 +57,8 @@ __device__ void block_fold(double (&v)[NREC], double *out) {
         double x = red[0][k];
         for (int q = 1; q < DIAG_T / WAVE; ++q) {
             const double y = red[q][k];
-            if (is_min(k)) x = fmin(x, y);
-            else if (is_max(k)) x = fmax(x, y);
+            if (is_min(k)) x = nmin(x, y);
+            else if (is_max(k)) x = nmax(x, y);
             else x += y;
         }
         out[k] = x;
@@ -85,10 +90,10 @@ __global__ void __launch_bounds__(DIAG_T) diag_partial_kernel(const T *__restric
                 const double p = (double)ps[l][r + i + 1];
                 const double px = (double)ps[l][r + i + 2] - p;   // forward differences (i+1 may be
                 const double py = (double)ps[l][rn + i + 1] - p;  // the ghost column, j+1 the ghost row)
-                v[ZMAX + l] = fmax(v[ZMAX + l], z);
-                v[ZMIN + l] = fmin(v[ZMIN + l], z);
-                v[PMAX + l] = fmax(v[PMAX + l], p);
-                v[PMIN + l] = fmin(v[PMIN + l], p);
+                v[ZMAX + l] = nmax(v[ZMAX + l], z);
+                v[ZMIN + l] = nmin(v[ZMIN + l], z);
+                v[PMAX + l] = nmax(v[PMAX + l], p);
+                v[PMIN + l] = nmin(v[PMIN + l], p);
                 v[ZSUM + l] += z;
                 v[ENS + l] += z * z;
                 v[KE + l] += px * px + py * py;
@@ -109,8 +114,8 @@ __global__ void __launch_bounds__(DIAG_T) diag_final_kernel(const double *part, 
         const double *q = part + (size_t)b * NREC;
 #pragma unroll
         for (int k = 0; k < NREC; ++k) {
-            if (is_min(k)) v[k] = fmin(v[k], q[k]);
-            else if (is_max(k)) v[k] = fmax(v[k], q[k]);
+            if (is_min(k)) v[k] = nmin(v[k], q[k]);
+            else if (is_max(k)) v[k] = nmax(v[k], q[k]);
             else v[k] += q[k];
         }
     }

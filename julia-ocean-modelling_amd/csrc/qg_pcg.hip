@@ -516,7 +516,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce_fast<4>(a, nblk_, 2, gathered_, s, gather, user));
         QG_HIP(hipMemcpyAsync(host, a.scal, sizeof(host), hipMemcpyDeviceToHost, s));
-        QG_HIP(hipStreamSynchronize(s));
+        QG_CHECK(comm_wait(user, s, nullptr, "PCG residual read"));
         iters_ = 1;
         bool done = true;
         for (int k = 0; k < 2; ++k) {
@@ -551,7 +551,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce_fast<2>(a, nblk_, 1, gathered_, s, gather, user));
         QG_HIP(hipMemcpyAsync(host, a.scal, sizeof(host), hipMemcpyDeviceToHost, s));
-        QG_HIP(hipStreamSynchronize(s));
+        QG_CHECK(comm_wait(user, s, nullptr, "PCG residual read"));
         iters_ = 1;
         bool done = true;
         for (int k = 0; k < 2; ++k) {
@@ -601,7 +601,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce(2, s, gather, user));
         QG_HIP(hipMemcpyAsync(host, a.scal, sizeof(host), hipMemcpyDeviceToHost, s));
-        QG_HIP(hipStreamSynchronize(s));
+        QG_CHECK(comm_wait(user, s, nullptr, "PCG residual read"));
         iters_ = it;
         static const bool trace = std::getenv("QG_PCG_TRACE") != nullptr;
         if (trace)

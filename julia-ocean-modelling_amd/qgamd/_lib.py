@@ -13,6 +13,9 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("QGMI355_LIB") or os.path.join(PKG_DIR, "lib", "libqgmi355.so")
 
 QG_OK = 0
+QG_ERR_INVALID_ARG, QG_ERR_UNSUPPORTED, QG_ERR_HIP, QG_ERR_NOT_BOUND = -1, -2, -3, -4
+QG_ERR_ALLOC, QG_ERR_RCCL, QG_ERR_NOT_CONVERGED = -5, -6, -7
+QG_XBUF_TO_NEXT, QG_XBUF_TO_PREV, QG_XBUF_FROM_PREV, QG_XBUF_FROM_NEXT = 0, 1, 2, 3
 QG_SOLVER_SPECTRAL = 0
 QG_F64, QG_F32 = 0, 1
 QG_SOLVER_PCG = 1
@@ -82,6 +85,8 @@ SIGNATURES = [
     ("qg_comm_unique_id", C.c_int, [C.c_char_p]),
     ("qg_comm_init", C.c_int, [_vp, C.c_int, C.c_int, C.c_char_p]),
     ("qg_comm_init_host", C.c_int, [_vp, C.c_int, C.c_int, AllgatherFn, SendrecvFn, _vp]),
+    ("qg_comm_set_timeout", C.c_int, [_vp, C.c_double]),
+    ("qg_comm_exchange_plan", C.c_int, [C.c_int, C.c_int, C.c_int * 2, C.c_int * 2, C.c_int * 2, C.c_int * 2]),
     ("qg_solver_create", C.c_int, [_i64, _i64, C.c_double, C.c_double * 2, C.c_int * 2,
                                    C.c_double * 4, C.c_double * 4, C.c_int, C.c_int, C.c_int, _vp,
                                    C.POINTER(_vp)]),

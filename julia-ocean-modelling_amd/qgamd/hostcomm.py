@@ -101,4 +101,110 @@ class TorchDistTransport:
 
         call("qg_comm_init_host", state._ctx, int(nranks), int(rank), self._ag, self._sr, None)
         state.rank, state.nranks = rank, nranks
+        state._attached_ranks = nranks
         state._transport = self  # keep the callbacks alive
+
+
+class ThreadRing:
+    """In-process ring of G ranks, one Python thread per rank, over qg_comm_init_host.
+
+    Every rank's State lives in this process (on one GPU or several); a grouped sendrecv or
+    an all-gather is a rendezvous of all G threads at a barrier, then device-to-device copies
+    straight between the ranks' staging buffers (no host bounce), then a second barrier so no
+    sender reuses a buffer before every receiver has copied it.  Messages between one pair of
+    ranks match in posting order, as with RCCL.  ctypes releases the GIL around the library
+    calls, so the G ranks' kernels overlap on the device.
+
+    Used to run the multi-rank path at workload size on the single GPU of a test box and to
+    compare the slabs with a single-GPU run of the same global model on the device, without
+    moving the fields through host memory.  A rank that fails (or a barrier not reached within
+    `timeout` seconds) breaks the barrier for all, and each callback returns non-zero, so every
+    rank's library call returns QG_ERR_RCCL instead of hanging.
+    """
+
+    def __init__(self, nranks, timeout=300.0):
+        import threading
+
+        self.G = nranks
+        self.timeout = timeout
+        self.barrier = threading.Barrier(nranks, timeout=timeout)
+        self.sends = [None] * nranks
+        self.gather = [None] * nranks
+        self._cb = []
+
+    def _wait(self):
+        self.barrier.wait()
+
+    def attach(self, state, rank):
+        from ._lib import call
+
+        h = hip()
+        h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        D2D = 3
+
+        def ag(user, send, recv, count, stream):
+            try:
+                if h.hipStreamSynchronize(stream) != 0:
+                    return 1
+                self.gather[rank] = (int(send), int(count))
+                self._wait()
+                for q, (ptr, n) in enumerate(self.gather):
+                    if n != count or h.hipMemcpy(int(recv) + 8 * q * count, ptr, 8 * count, D2D) != 0:
+                        return 1
+                self._wait()
+                return 0
+            except Exception as e:  # includes threading.BrokenBarrierError
+                self.barrier.abort()
+                print(f"ThreadRing rank {rank}: allgather failed: {e!r}", flush=True)
+                return 1
+
+        def sr(user, ns, sp, sc, speer, nr, rp, rc, rpeer, stream):
+            try:
+                if h.hipStreamSynchronize(stream) != 0:
+                    return 1
+                self.sends[rank] = [(int(speer[k]), int(sp[k]), int(sc[k])) for k in range(ns)]
+                self._wait()
+                taken = {}
+                for k in range(nr):
+                    peer = int(rpeer[k])
+                    n = taken.get(peer, 0)  # the n-th message this rank takes from `peer`
+                    taken[peer] = n + 1
+                    mine = [m for m in self.sends[peer] if m[0] == rank]
+                    _, ptr, cnt = mine[n]
+                    if cnt != rc[k] or h.hipMemcpy(int(rp[k]), ptr, 8 * cnt, D2D) != 0:
+                        return 1
+                self._wait()
+                return 0
+            except Exception as e:
+                self.barrier.abort()
+                print(f"ThreadRing rank {rank}: sendrecv failed: {e!r}", flush=True)
+                return 1
+
+        agf, srf = AllgatherFn(ag), SendrecvFn(sr)
+        self._cb.append((agf, srf))
+        call("qg_comm_init_host", state._ctx, int(self.G), int(rank), agf, srf, None)
+        state.rank, state.nranks = rank, self.G
+        state._attached_ranks = self.G
+        state._transport = self
+
+    @staticmethod
+    def run_all(fns):
+        """Run fns[r]() on G threads; re-raise the first exception."""
+        import threading
+
+        errs = [None] * len(fns)
+
+        def body(r):
+            try:
+                fns[r]()
+            except BaseException as e:  # noqa: BLE001 -- reported below
+                errs[r] = e
+
+        ts = [threading.Thread(target=body, args=(r,)) for r in range(len(fns))]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for e in errs:
+            if e is not None:
+                raise e

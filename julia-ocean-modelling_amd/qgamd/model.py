@@ -193,19 +193,32 @@ class State:
         torch = _torch()
         self.model = m
         self.P_local = m.P if P_local is None else P_local
-        self.device = torch.cuda.current_device() if device is None else device
+        # device: None (current), an ordinal, "cuda:k" or a torch.device -> ordinal k.  The
+        # arrays and the stream the library launches on all belong to that device.
+        if device is None:
+            self.device = torch.cuda.current_device()
+        else:
+            dev = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+            if dev.type != "cuda":
+                raise ValueError(f"State needs a CUDA (HIP) device, got {dev}")
+            self.device = dev.index if dev.index is not None else torch.cuda.current_device()
         self.dtype = torch.float64 if dtype is None else dtype
         if self.dtype not in (torch.float64, torch.float32):
             raise ValueError("dtype must be torch.float64 or torch.float32")
-        self.zeta = device_zeros(m, self.P_local, dtype=self.dtype)
-        self.psi = device_zeros(m, self.P_local, dtype=self.dtype)
-        self.f_store = device_zeros(m, self.P_local, dtype=self.dtype)
-        self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local, precond, pcg_rtol, pcg_maxit,
-                                _lib.QG_F32 if self.dtype == torch.float32 else _lib.QG_F64, wind)
-        self._ctx = C.c_void_p()
-        call("qg_create", C.byref(self.params), int(self.device), _stream_ptr(), C.byref(self._ctx))
-        call("qg_bind_state", self._ctx, _ptr(self.zeta), _ptr(self.psi), _ptr(self.f_store))
+        with torch.cuda.device(self.device):
+            dev = torch.device("cuda", self.device)
+            self.zeta = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
+            self.psi = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
+            self.f_store = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
+            self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local, precond, pcg_rtol, pcg_maxit,
+                                    _lib.QG_F32 if self.dtype == torch.float32 else _lib.QG_F64, wind)
+            self._ctx = C.c_void_p()
+            call("qg_create", C.byref(self.params), int(self.device), _stream_ptr(), C.byref(self._ctx))
+            call("qg_bind_state", self._ctx, _ptr(self.zeta), _ptr(self.psi), _ptr(self.f_store))
+        # rank / nranks describe the slab this state holds (e.g. read back from a slab
+        # checkpoint); stepping a slab of a multi-rank run needs that transport attached first
         self.rank, self.nranks = rank, nranks
+        self._attached_ranks = 1
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
@@ -217,6 +230,12 @@ class State:
     def comm_init(self, nranks, rank, uid: bytes):
         call("qg_comm_init", self._ctx, int(nranks), int(rank), C.c_char_p(uid))
         self.rank, self.nranks = rank, nranks
+        self._attached_ranks = nranks
+
+    def _need_transport(self):
+        if self.nranks != self._attached_ranks:
+            raise RuntimeError(f"this state is slab {self.rank} of {self.nranks}: attach the {self.nranks}-rank "
+                               "transport (comm_init / TorchDistTransport.attach) before stepping it")
 
     # -- reference operations ----------------------------------------------------------
     def initialise(self, seeds=(SEED_LAYER1, SEED_LAYER2)):
@@ -224,15 +243,19 @@ class State:
         return self
 
     def evolve_zeta_(self, timestep):
+        self._need_transport()
         call("qg_evolve_zeta", self._ctx, int(timestep))
 
     def evolve_psi_(self):
+        self._need_transport()
         call("qg_evolve_psi", self._ctx)
 
     def step(self, timestep):
+        self._need_transport()
         call("qg_step", self._ctx, int(timestep))
 
     def run(self, first_step, nsteps):
+        self._need_transport()
         call("qg_run", self._ctx, int(first_step), int(nsteps))
 
     def synchronize(self):

@@ -71,3 +71,18 @@ def test_run_model_monitor(env, tmp_path):
                     monitor=lambda t, d: seen.append((t, qgamd.update_max(-np.inf, d["psi_max"][0]))))
     assert [t for t, _ in seen] == [0, 8, 16]
     assert all(np.isfinite(v) for _, v in seen)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_nan_propagates_to_extrema(env, dtype):
+    """A diverged state must not report finite extrema: Julia's maximum / minimum (what
+    update_max / update_min of run_model.jl:41-53 fold) return NaN when the matrix holds one."""
+    torch, qgamd, _ = env
+    kw = {} if dtype == "f64" else {"dtype": torch.float32}
+    st = qgamd.initialise_model(qgamd.bench_model(64, P=48), **kw)
+    st.current("zeta", 2)[17, 23] = float("nan")  # layer 2 only
+    st.synchronize()
+    d = st.diagnostics()
+    assert np.isnan(d["zeta_max"][1]) and np.isnan(d["zeta_min"][1])
+    assert np.isfinite(d["zeta_max"][0]) and np.isfinite(d["zeta_min"][0])
+    assert np.all(np.isfinite(d["psi_max"])) and np.all(np.isfinite(d["psi_min"]))

@@ -105,3 +105,41 @@ def test_widest_rows_8192(env, P, kw):
     ref = O.State(R.bench_model(8192, P=P, dt=60.0)).run(3)
     for n in ("psi", "zeta"):
         assert rel(st.to_numpy(n), getattr(ref, n)) < TOL, n
+
+
+def test_attach_after_single_rank_seed_is_refused():
+    """qg_initialise seeds the noise from global row offsets (rank, nranks): attaching a
+    multi-rank transport to a state seeded as one rank would step the wrong initial field,
+    so the library refuses it (QG_ERR_INVALID_ARG); seeding after the attach works."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ctypes as C
+    import qgamd
+    from qgamd import _lib
+
+    m = qgamd.bench_model(32, P=32)
+    st = qgamd.State(m, P_local=16).initialise()
+    noop_ag = _lib.AllgatherFn(lambda *a: 0)
+    noop_sr = _lib.SendrecvFn(lambda *a: 0)
+    rc = _lib.lib().qg_comm_init_host(st._ctx, 2, 0, noop_ag, noop_sr, None)
+    assert rc == _lib.QG_ERR_INVALID_ARG
+
+
+def test_slab_checkpoint_needs_its_transport(tmp_path):
+    """A slab of a multi-rank run read back from its checkpoint refuses to step until the
+    transport of that many ranks is attached (it would otherwise run as a periodic domain)."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+
+    st = qgamd.State(qgamd.bench_model(32), device=torch.device("cuda", 0)).initialise()
+    st.run(1, 2)
+    st.rank, st.nranks = 1, 2  # pretend it is slab 1 of 2
+    path = str(tmp_path / "ck.npz")
+    qgamd.save_checkpoint(st, path, 2)
+    st2, t = qgamd.load_checkpoint(path, device="cuda:0")
+    assert (st2.rank, st2.nranks, t) == (1, 2, 3)
+    with pytest.raises(RuntimeError, match="transport"):
+        st2.run(t, 1)

@@ -1,10 +1,14 @@
 #!/bin/bash
-# one GPU round: parity tests, bench, rocprof kernel stats.  usage: tools/gpu_check.sh TAG [bench args]
+# one GPU round: parity tests, bench (driver flags and defaults), rocprof kernel stats.
+# usage: tools/gpu_check.sh TAG [extra bench args]
 TAG=$1; shift
 R=$GRAFT_REPO_ROOT
 cd $R || exit 1
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/tests_$TAG.log 2>&1
+mkdir -p gpurun_out
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
 rc=$?; tail -3 gpurun_out/tests_$TAG.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python bench.py --warmup 5 --steps 20 "$@" > gpurun_out/bench_${TAG}_drv.json 2> gpurun_out/bench_${TAG}_drv.err || exit 3
+cat gpurun_out/bench_${TAG}_drv.json
 timeout -k 10 600 python bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit 3
 cat gpurun_out/bench_$TAG.json
 cd /tmp && export TMPDIR=/tmp
