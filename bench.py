@@ -73,6 +73,9 @@ def parse():
                     help="N > 1: RCCL over xGMI (default), or the host transport over gloo -- a "
                          "rehearsal of the multi-rank bench with several ranks on one GPU (slow, "
                          "not a measurement)")
+    ap.add_argument("--overlap", action="store_true",
+                    help="N > 1 (or --comm-self): post the halo exchange on a second stream while the "
+                         "interior rows' tendency runs (qg_set_overlap; bit-identical results)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
@@ -188,6 +191,8 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         st.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
+    if args.overlap:
+        st.set_overlap(True)
     st.initialise()
     torch.cuda.synchronize()
     setup_ms = (time.perf_counter() - t_setup) * 1e3
@@ -323,6 +328,7 @@ def main():
                        else "matrix-free PCG on the 5-point operator, spectral preconditioner"),
             "finite": finite,
             "transport": (args.transport if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
+            "halo_overlap": bool(args.overlap and (world > 1 or args.comm_self)),
         },
         "roofline": {
             "bound": "hbm",

@@ -205,6 +205,14 @@ int qg_comm_init_host(qg_ctx *ctx, int nranks, int rank, qg_allgather_fn allgath
  * Julia process with no failure handling; this guards the multi-GPU path only.)         */
 #define QG_PACE_STEPS 16
 int qg_comm_set_timeout(qg_ctx *ctx, double seconds);
+/* Halo / interior overlap (north_star: "halo exchange overlapped with interior compute").
+ * on = 1: each multi-rank evolve_zeta posts the halo exchange (pack, send/recv, unpack) on a
+ * second HIP stream and runs the tendency of the interior rows j in [2, P-2), which need no
+ * halo, on the context's stream meanwhile; the four boundary rows follow after an event
+ * wait.  Bit-identical to on = 0 (the per-point arithmetic does not depend on the launch
+ * geometry).  Default: the environment variable QG_OVERLAP (read at qg_create), else 0.
+ * No effect on a single GPU (no exchange) or for P < 8 (no interior worth splitting).   */
+int qg_set_overlap(qg_ctx *ctx, int on);
 /* The posting schedule of one halo exchange on `rank` of a ring of `nranks` y-slabs, as the
  * library issues it (RCCL: one ncclGroupStart/End; host transport: one sendrecv call):
  * sends k = 0, 1 go to send_peer[k] from buffer send_buf[k], receives k = 0, 1 come from

@@ -74,6 +74,10 @@ struct qg_ctx {
     bool graph_ok = true;  // cleared if capture fails (then qg_run launches step by step)
     hipStream_t gstream = nullptr;
     hipEvent_t gev_in = nullptr, gev_out = nullptr;
+    // halo / interior overlap (qg_set_overlap): exchange stream, "fields ready" and "halo in"
+    bool overlap = false;
+    hipStream_t ov_stream = nullptr;
+    hipEvent_t ov_ready = nullptr, ov_halo = nullptr;
     hipEvent_t pace_ev = nullptr;  // multi-GPU pacing (qg_step)
     bool pace_armed = false;
     int64_t pace_count = 0;
@@ -203,6 +207,7 @@ int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out) {
         delete c;
         return st;
     }
+    if (const char *e = std::getenv("QG_OVERLAP")) c->overlap = std::atoi(e) != 0;
     *out = c;
     return QG_OK;
 }
@@ -215,8 +220,12 @@ int qg_destroy(qg_ctx *c) {
     if (c->snap_ready) (void)hipEventDestroy(c->snap_ready);
     if (c->snap_done) (void)hipEventDestroy(c->snap_done);
     if (c->snap_stream) (void)hipStreamDestroy(c->snap_stream);
+    if (c->ov_stream) (void)hipStreamSynchronize(c->ov_stream);
     if (c->comm) comm_destroy(c->comm);
     if (c->halo) (void)hipFree(c->halo);
+    if (c->ov_stream) (void)hipStreamDestroy(c->ov_stream);
+    if (c->ov_ready) (void)hipEventDestroy(c->ov_ready);
+    if (c->ov_halo) (void)hipEventDestroy(c->ov_halo);
     if (c->diag) (void)hipFree(c->diag);
     if (c->wind) (void)hipFree(c->wind);
     drop_graphs(c);
@@ -350,8 +359,6 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
         // (the f2 fields are the newest psi and zeta: their ghost rows come from the halo rows)
         double *f1[2] = {c->field(c->fst, 0, fh), c->field(c->fst, 1, fh)};
         const int n1 = c->ghosts_pending ? 2 : 0;
-        QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, c->row_words(), p.P, c->stream, c->ghosts_pending));
-        c->ghosts_pending = false;
         const int64_t row = p.M + 2;  // halo buffer: [field][4 rows][M+2 elements]; +1 = interior start
         const T *hb = reinterpret_cast<const T *>(c->halo);
         for (int l = 0; l < 2; ++l)
@@ -359,7 +366,40 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
                 a.psi_rows[l].halo[h] = hb + ((size_t)(l * 4 + h)) * row + 1;
                 a.zeta_rows[l].halo[h] = hb + ((size_t)((2 + l) * 4 + h)) * row + 1;
             }
-        QG_CHECK(launch_tendency(a, c->stream));
+        if (c->overlap && p.P >= 8) {
+            // exchange on the side stream, ordered after everything already queued on the
+            // context's stream (the previous step's pass B, a ghost flush using the staging
+            // buffer); the interior rows [2, P-2) read only local rows -- no halo, no ghost
+            // row -- and write rows the unpack never touches, so they run meanwhile
+            if (!c->ov_stream) {
+                QG_HIP(hipStreamCreateWithFlags(&c->ov_stream, hipStreamNonBlocking));
+                QG_HIP(hipEventCreateWithFlags(&c->ov_ready, hipEventDisableTiming));
+                QG_HIP(hipEventCreateWithFlags(&c->ov_halo, hipEventDisableTiming));
+            }
+            QG_HIP(hipEventRecord(c->ov_ready, c->stream));
+            QG_HIP(hipStreamWaitEvent(c->ov_stream, c->ov_ready, 0));
+            QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, c->row_words(), p.P, c->ov_stream,
+                                   c->ghosts_pending));
+            QG_HIP(hipEventRecord(c->ov_halo, c->ov_stream));
+            c->ghosts_pending = false;
+            TendArgsT<T> in = a;
+            in.j0 = 2;
+            in.j1 = (int)p.P - 2;
+            in.j2 = in.j3 = 0;
+            QG_CHECK(launch_tendency(in, c->stream));
+            QG_HIP(hipStreamWaitEvent(c->stream, c->ov_halo, 0));
+            TendArgsT<T> bd = a;  // rows 0, 1 and P-2, P-1: one launch, two row ranges
+            bd.j0 = 0;
+            bd.j1 = 2;
+            bd.j2 = (int)p.P - 2;
+            bd.j3 = (int)p.P;
+            QG_CHECK(launch_tendency(bd, c->stream));
+        } else {
+            QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, c->row_words(), p.P, c->stream,
+                                   c->ghosts_pending));
+            c->ghosts_pending = false;
+            QG_CHECK(launch_tendency(a, c->stream));
+        }
         c->ghosts_pending = true;
     }
     c->heads[0] = zn;
@@ -645,6 +685,12 @@ int qg_synchronize(qg_ctx *c) {
 }
 
 // ---- multi-GPU -------------------------------------------------------------------------
+int qg_set_overlap(qg_ctx *c, int on) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    c->overlap = on != 0;
+    return QG_OK;
+}
+
 int qg_comm_set_timeout(qg_ctx *c, double seconds) {
     if (!c || !(seconds > 0)) return QG_ERR_INVALID_ARG;
     if (!c->comm) return QG_ERR_RCCL;

@@ -134,6 +134,59 @@ solver here, so the handles are accepted for signature compatibility and ignored
 evolve_psi!(model, s::QGState, poisson=nothing, helmholtz=nothing) =
     @qgcheck qg_evolve_psi ccall((:qg_evolve_psi, libqg), Cint, (Ptr{Cvoid},), s.ctx)
 
+# --- the reference's exact array signatures (model.jl:155, :172) -------------------------
+# A caller that keeps the reference's own loop (`evolve_zeta!(model, zeta, psi, t, f_store)`
+# then `evolve_psi!(model, zeta, psi, P, H)`) on device arrays gets a library context bound to
+# those arrays, created on first use and cached by the arrays' addresses.  Each call leaves
+# the arrays in the reference's slot order (slot 1 = newest), as store_new_state! does, so
+# `zeta[:, :, 1, 1]` means what it means in the reference.  (The rotation-free fast path is
+# QGState / run_model_no_output.)
+const _BOUND = Dict{NTuple{3,UInt},QGState}()
+
+function _bound_state(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, f_store::ROCArray{T,4}) where {T}
+    size(zeta) == size(psi) == size(f_store) == (model.M + 2, model.P + 2, 2, 3) ||
+        throw(DimensionMismatch("zeta, psi, f_store must be (M+2, P+2, 2, 3)"))
+    key = (UInt(pointer(zeta)), UInt(pointer(psi)), UInt(pointer(f_store)))
+    get!(_BOUND, key) do
+        params = Ref(QGParams(model; dtype=T))
+        ctx = Ref{Ptr{Cvoid}}(C_NULL)
+        @qgcheck qg_create ccall((:qg_create, libqg), Cint, (Ptr{QGParams}, Cint, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                                 params, AMDGPU.device_id(AMDGPU.device()) - 1, stream_ptr(), ctx)
+        @qgcheck qg_bind_state ccall((:qg_bind_state, libqg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
+                                     ctx[], pointer(zeta), pointer(psi), pointer(f_store))
+        s = QGState{T}(ctx[], zeta, psi, f_store)
+        finalizer(x -> ccall((:qg_destroy, libqg), Cint, (Ptr{Cvoid},), x.ctx), s)
+        s
+    end
+end
+
+"""`evolve_zeta!(model, zeta, psi, timestep, f_store)` — model.jl:155 with its signature."""
+function evolve_zeta!(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, timestep::Integer,
+                      f_store::ROCArray{T,4}) where {T<:Union{Float64,Float32}}
+    s = _bound_state(model, zeta, psi, f_store)
+    evolve_zeta!(model, s, timestep)
+    canonical!(s)
+    nothing
+end
+
+"""`evolve_psi!(model, zeta, psi, poisson_cholesky, helmholtz_cholesky)` — model.jl:172 with
+its signature; the factor arguments are accepted and the bound context's solver is used."""
+function evolve_psi!(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, poisson=nothing,
+                     helmholtz=nothing) where {T<:Union{Float64,Float32}}
+    key_match = [s for (k, s) in _BOUND if k[1] == UInt(pointer(zeta)) && k[2] == UInt(pointer(psi))]
+    isempty(key_match) && throw(ArgumentError("evolve_psi!: call evolve_zeta! on these arrays first " *
+                                              "(it binds them with their f_store)"))
+    s = only(key_match)
+    evolve_psi!(model, s)
+    canonical!(s)
+    nothing
+end
+
+"""`set_overlap!(s, on)`: multi-rank halo exchange on a second stream while the interior rows'
+tendency runs (bit-identical; include/qg_mi355.h qg_set_overlap)."""
+set_overlap!(s::QGState, on::Bool=true) =
+    @qgcheck qg_set_overlap ccall((:qg_set_overlap, libqg), Cint, (Ptr{Cvoid}, Cint), s.ctx, Cint(on))
+
 """`run_model_no_output(model)` (run_model_no_output.jl:3-16) -> (zeta, psi) on the device,
 slots in the reference's order."""
 function run_model_no_output(model; kw...)

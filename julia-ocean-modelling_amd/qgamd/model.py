@@ -185,10 +185,12 @@ class State:
 
     def __init__(self, m, solver=_lib.QG_SOLVER_SPECTRAL, P_fwd=None, chunk_rows=0,
                  device=None, rank=0, nranks=1, P_local=None, precond=_lib.QG_PRECOND_SPECTRAL,
-                 pcg_rtol=1e-12, pcg_maxit=500, dtype=None, wind=None):
+                 pcg_rtol=1e-12, pcg_maxit=500, dtype=None, wind=None, arrays=None):
         """dtype: torch.float64 (default, the reference's arithmetic) or torch.float32 (the
         F32 state of BASELINE config 5; spectral solver only).  wind: (tau0, rho0) of the
-        wind-forcing extension, or None (the reference's right-hand side)."""
+        wind-forcing extension, or None (the reference's right-hand side).  arrays: an
+        existing (zeta, psi, f_store) triple of (3, 2, P+2, M+2) device tensors to bind
+        instead of allocating new ones (the caller keeps ownership)."""
         _lib.lib()  # the HIP library first: no CPU fallback, fail before touching the device
         torch = _torch()
         self.model = m
@@ -207,9 +209,18 @@ class State:
             raise ValueError("dtype must be torch.float64 or torch.float32")
         with torch.cuda.device(self.device):
             dev = torch.device("cuda", self.device)
-            self.zeta = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
-            self.psi = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
-            self.f_store = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
+            if arrays is None:
+                self.zeta = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
+                self.psi = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
+                self.f_store = device_zeros(m, self.P_local, device=dev, dtype=self.dtype)
+            else:
+                shape = (3, 2, self.P_local + 2, m.M + 2)
+                for t in arrays:
+                    if (tuple(t.shape) != shape or t.dtype != self.dtype or t.device != dev
+                            or not t.is_contiguous()):
+                        raise ValueError(f"bound arrays must be contiguous {self.dtype} tensors of shape "
+                                         f"{shape} on {dev}")
+                self.zeta, self.psi, self.f_store = arrays
             self.params = qg_params(m, solver, P_fwd, chunk_rows, self.P_local, precond, pcg_rtol, pcg_maxit,
                                     _lib.QG_F32 if self.dtype == torch.float32 else _lib.QG_F64, wind)
             self._ctx = C.c_void_p()
@@ -231,6 +242,11 @@ class State:
         call("qg_comm_init", self._ctx, int(nranks), int(rank), C.c_char_p(uid))
         self.rank, self.nranks = rank, nranks
         self._attached_ranks = nranks
+
+    def set_overlap(self, on=True):
+        """qg_set_overlap: post each step's halo exchange on a second stream and run the
+        interior rows' tendency meanwhile (multi-rank only; bit-identical results)."""
+        call("qg_set_overlap", self._ctx, 1 if on else 0)
 
     def _need_transport(self):
         if self.nranks != self._attached_ranks:
@@ -320,9 +336,34 @@ def initialise_model(m, seeds=(SEED_LAYER1, SEED_LAYER2), **kw):
     return State(m, **kw).initialise(seeds)
 
 
-def evolve_zeta_(m, state, timestep):
-    """evolve_zeta!(model, zeta, psi, timestep, f_store) (model.jl:155-158)."""
-    state.evolve_zeta_(timestep)
+_BOUND = {}
+
+
+def _bound_state(m, zeta, psi, f_store):
+    """The library context bound to a caller's (zeta, psi, f_store) arrays, created on first
+    use and cached by their addresses (the reference-signature calls below)."""
+    key = (zeta.data_ptr(), psi.data_ptr(), f_store.data_ptr())
+    st = _BOUND.get(key)
+    if st is None or st.model != m:
+        st = _BOUND[key] = State(m, device=zeta.device, dtype=zeta.dtype, arrays=(zeta, psi, f_store))
+    return st
+
+
+def evolve_zeta_(m, *args):
+    """evolve_zeta!(model, zeta, psi, timestep, f_store) (model.jl:155-158).
+
+    Two forms: ``evolve_zeta_(m, state, timestep)`` on a :class:`State` (slots rotate, no
+    copies), and the reference's own signature ``evolve_zeta_(m, zeta, psi, timestep,
+    f_store)`` on (3, 2, P+2, M+2) device tensors, which leaves the arrays in the reference's
+    slot order after the call (slot 1 = newest, as store_new_state! leaves them)."""
+    if len(args) == 2:
+        state, timestep = args
+        state.evolve_zeta_(timestep)
+        return
+    zeta, psi, timestep, f_store = args
+    st = _bound_state(m, zeta, psi, f_store)
+    st.evolve_zeta_(timestep)
+    st.canonicalize()
 
 
 class SolverHandle:
@@ -341,14 +382,30 @@ def get_helmholtz_cholesky(M, P, dx, alpha):  # laplacian.jl:60-64
     return SolverHandle("helmholtz", M, P, dx, alpha)
 
 
-def evolve_psi_(m, state, poisson=None, helmholtz=None):
-    """evolve_psi!(model, zeta, psi, poisson_cholesky, helmholtz_cholesky) (model.jl:172-199)."""
+def evolve_psi_(m, *args):
+    """evolve_psi!(model, zeta, psi, poisson_cholesky, helmholtz_cholesky) (model.jl:172-199).
+
+    ``evolve_psi_(m, state[, poisson, helmholtz])`` on a :class:`State`, or the reference's
+    signature ``evolve_psi_(m, zeta, psi, poisson, helmholtz)`` on device tensors already
+    bound by :func:`evolve_zeta_` (which knows their f_store)."""
+    if isinstance(args[0], State):
+        state, poisson, helmholtz = (tuple(args) + (None, None))[:3]
+        canonical = False
+    else:
+        zeta, psi, poisson, helmholtz = args
+        hits = [st for k, st in _BOUND.items() if k[:2] == (zeta.data_ptr(), psi.data_ptr())]
+        if len(hits) != 1:
+            raise ValueError("evolve_psi_: call evolve_zeta_ on these arrays first (it binds them "
+                             "with their f_store)")
+        state, canonical = hits[0], True
     for h, kind in ((poisson, "poisson"), (helmholtz, "helmholtz")):
         if h is not None and (h.kind != kind or h.M != m.M or h.P != m.P or h.dx != m.dx):
             raise ValueError(f"{kind} handle does not match the model")
     if helmholtz is not None and helmholtz.alpha != S_eig(m):
         raise ValueError("helmholtz handle alpha != S_eig(model)")
     state.evolve_psi_()
+    if canonical:
+        state.canonicalize()
 
 
 def run_model_no_output(m, nsteps=None, seeds=(SEED_LAYER1, SEED_LAYER2), **kw):

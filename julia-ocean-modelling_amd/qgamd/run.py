@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import json
+import re
 import time
 import zipfile
 
@@ -37,23 +38,63 @@ def create_metadata(m):
             "total_steps": int(np.floor(m.T / m.dt))}
 
 
+def julia_repr(x) -> str:
+    """``print(x::Float64)`` as Julia writes it (Base.Ryu.writeshortest, compact=false):
+    the shortest round-trip digits (the same digits as Python's ``repr``), in decimal form
+    when the decimal point position ``pt`` satisfies -4 < pt <= 6 and otherwise as
+    ``d.ddde±n`` — e.g. ``4.0e6``, ``1.0e-6``, ``123456.0``, ``0.0001``, ``2.52288e8``.
+    Integers print as themselves."""
+    if isinstance(x, (int, np.integer)) and not isinstance(x, bool):
+        return str(int(x))
+    x = float(x)
+    if x != x:
+        return "NaN"
+    if x in (float("inf"), float("-inf")):
+        return "Inf" if x > 0 else "-Inf"
+    if x == 0.0:
+        return "-0.0" if str(x).startswith("-") else "0.0"
+    sign = "-" if x < 0 else ""
+    r = repr(abs(x))  # shortest round-trip digits
+    m = re.fullmatch(r"(\d+)(?:\.(\d*))?(?:e([+-]?\d+))?", r)
+    ip, fp, ex = m.group(1), m.group(2) or "", int(m.group(3) or 0)
+    digits = (ip + fp).lstrip("0")
+    # decimal exponent of the digit string: value = 0.digits * 10^pt
+    lead_zeros = len(ip + fp) - len((ip + fp).lstrip("0"))
+    pt = len(ip) + ex - lead_zeros
+    digits = digits.rstrip("0") or "0"
+    olength = len(digits)
+    nexp = pt - olength  # value = digits * 10^nexp
+    if -4 < pt <= 6 and not (pt >= olength and abs((abs(x) + 0.05) % 10.0 ** (pt - olength) - 0.05) > 0.05):
+        if pt <= 0:
+            body = "0." + "0" * (-pt) + digits
+        elif pt >= olength:
+            body = digits + "0" * (pt - olength) + ".0"
+        else:
+            body = digits[:pt] + "." + digits[pt:]
+    else:
+        body = digits[0] + "." + (digits[1:] or "0") + "e" + str(nexp + olength - 1)
+    return sign + body
+
+
 def log_model_params(m, out=print):
-    """run_model.jl:22-39 (same lines, same order)."""
+    """run_model.jl:22-39 (same lines, same order; numbers printed as Julia's ``println``
+    prints a Float64 / Int, see :func:`julia_repr`)."""
     total_steps = int(np.floor(m.T / m.dt))
+    j = julia_repr
     out("Parameters:")
-    out(f"Lx = {m.Lx}")
-    out(f"Ly = {m.Ly}")
-    out(f"(f_0^2 / N^2): {ratio_term(m)}")
-    out(f"S1 = {S1_plus(m)}")
-    out(f"S2 = {S2_minus(m)}")
-    out(f"Beta_1 = {beta_1(m)}")
-    out(f"Beta_2 = {beta_2(m)}")
-    out(f"M = {m.M}")
-    out(f"P = {m.P}")
-    out(f"dt = {m.dt}")
-    out(f"T = {m.T}")
-    out(f"U = {m.U}")
-    out(f"Initial kick = {m.initial_kick}")
+    out(f"Lx = {j(m.Lx)}")
+    out(f"Ly = {j(m.Ly)}")
+    out(f"(f_0^2 / N^2): {j(ratio_term(m))}")
+    out(f"S1 = {j(S1_plus(m))}")
+    out(f"S2 = {j(S2_minus(m))}")
+    out(f"Beta_1 = {j(beta_1(m))}")
+    out(f"Beta_2 = {j(beta_2(m))}")
+    out(f"M = {j(m.M)}")
+    out(f"P = {j(m.P)}")
+    out(f"dt = {j(m.dt)}")
+    out(f"T = {j(m.T)}")
+    out(f"U = {j(m.U)}")
+    out(f"Initial kick = {j(m.initial_kick)}")
     out(f"Total steps = {total_steps}\n")
 
 

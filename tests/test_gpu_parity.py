@@ -224,6 +224,32 @@ def test_evolve_functions_match_step(torch, qg):
     assert np.array_equal(a.psi.permute(3, 2, 1, 0).cpu().numpy(), before)
 
 
+def test_reference_array_signatures(torch, qg, O, R):
+    """The reference's own loop on bare arrays: evolve_zeta!(model, zeta, psi, t, f_store),
+    evolve_psi!(model, zeta, psi, P, H) (model.jl:155, :172), slot 1 = newest after every call
+    (as store_new_state! leaves it) — equal to qg_step, and the oracle after 4 steps."""
+    m = qg.bench_model(48, P=32)
+    ref = qg.initialise_model(m)
+    ref.canonicalize()
+    zeta, psi, f_store = ref.zeta.clone(), ref.psi.clone(), ref.f_store.clone()
+    pc = qg.get_poisson_cholesky(m.M, m.P, m.dx)
+    hc = qg.get_helmholtz_cholesky(m.M, m.P, m.dx, qg.S_eig(m))
+    z0 = zeta[0].clone()
+    for t in range(1, 5):
+        qg.evolve_zeta_(m, zeta, psi, t, f_store)
+        if t == 1:  # slot 2 now holds the initial field, shifted down by store_new_state!
+            assert torch.equal(zeta[1], z0) and not torch.equal(zeta[0], z0)
+        qg.evolve_psi_(m, zeta, psi, pc, hc)
+        ref.step(t)
+        ref_z, ref_p, ref_f = ref.logical("zeta"), ref.logical("psi"), ref.logical("f_store")
+        assert torch.equal(zeta, ref_z) and torch.equal(psi, ref_p) and torch.equal(f_store, ref_f)
+    oracle = O.State(R.bench_model(48, P=32)).run(4)
+    got = psi.permute(3, 2, 1, 0).cpu().numpy()
+    assert rel(got[:, :, :, 0], oracle.psi[:, :, :, 0]) < TOL
+    with pytest.raises(ValueError):
+        qg.evolve_psi_(m, psi, zeta, pc, hc)  # arrays never bound by evolve_zeta_
+
+
 @pytest.mark.parametrize("N,steps", [(128, 100), (256, 20)])
 def test_long_run_against_c_oracle(torch, qg, O, R, N, steps):
     m = qg.bench_model(N)

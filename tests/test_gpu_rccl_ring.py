@@ -10,7 +10,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def test_one_rank_rccl_ring_matches_single_gpu():
+@pytest.mark.parametrize("overlap", [False, True])
+def test_one_rank_rccl_ring_matches_single_gpu(overlap):
+    """overlap: the halo exchange (RCCL send/recv to self) on the second stream while the
+    interior rows' tendency runs -- bitwise equal to the default schedule."""
     import torch
 
     if not torch.cuda.is_available():
@@ -23,9 +26,19 @@ def test_one_rank_rccl_ring_matches_single_gpu():
     uid = C.create_string_buffer(128)
     qgamd._lib.call("qg_comm_unique_id", uid)
     st.comm_init(1, 0, uid.raw)
+    st.set_overlap(overlap)
     st.initialise()
     st.run(1, 7)
     torch.cuda.synchronize()
     for n in ("zeta", "psi", "f_store"):
         a, b = st.to_numpy(n), ref.to_numpy(n)
         assert np.linalg.norm(a - b) / np.linalg.norm(b) < 1e-13, n
+    if overlap:  # same ring without the overlap: bit for bit
+        st2 = qgamd.State(m)
+        uid2 = C.create_string_buffer(128)
+        qgamd._lib.call("qg_comm_unique_id", uid2)
+        st2.comm_init(1, 0, uid2.raw)
+        st2.initialise()
+        st2.run(1, 7)
+        for n in ("zeta", "psi", "f_store"):
+            assert np.array_equal(st.to_numpy(n), st2.to_numpy(n)), n
