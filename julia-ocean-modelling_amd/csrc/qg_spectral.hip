@@ -1,6 +1,7 @@
 // Spectral (FACR) direct solver kernels for gfx950 -- see qg_spectral.hpp for the method.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -189,9 +190,9 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                     const double2 B[2] = {make_double2(Zk.x, Zn.x), make_double2(Zk.y, Zn.y)};
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
-                        const int o0 = s * KS, oN = s * KS + NH;
+                        const int o0 = s * KS;
                         const double r0 = QG_PA_R(q, s, o0), rN = crN[s];
-                        (void)oN;
+                        (void)o0;
                         u[q][s] = make_double2((r0 * a.csc) * B[s].x + r0 * u[q][s].x,
                                                (rN * a.csc) * B[s].y + rN * u[q][s].y);
                         Urow[s * KS] = Store<S>::c(make_double2(u[q][s].x, 0));
@@ -1529,6 +1530,275 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// Split passes: rows that are not a power of two and too wide for the generic passes
+// (GEN_MMAX < M <= SPL_MMAX).  Three row buffers no longer fit in LDS, and the recurrence
+// state of every wavenumber of a chunk no longer fits in one workgroup's registers, so the
+// row transform and the y-recurrences become separate kernels:
+//   spec_fft_split<fwd>: per row, project + M-point DFT in place in ONE LDS buffer (mixed-radix
+//                        decimation-in-frequency stages, output in digit-reversed order, or a
+//                        direct DFT for rows with a prime factor > 13), split into the two
+//                        systems' spectra B_s(k), stored in U;
+//   spec_passA_split:    one thread per (chunk, wavenumber): backward filter over the chunk's
+//                        rows, u in place of B in U, chunk summaries (the generic pass A's
+//                        arithmetic, in the same order);
+//   spec_carry / spec_pin: unchanged;
+//   spec_passB_split:    one thread per (chunk, wavenumber): carries, forward filter, X_s(k)
+//                        in place of u in U (the generic pass B's arithmetic);
+//   spec_fft_split<inv>: per row, rebuild the M-point spectrum from X_0, X_1, inverse DFT,
+//                        pin, back-projection, store with ghosts.
+// Twice the generic passes' traffic (U makes three round trips instead of one), but any
+// M <= 8192 works: the capability path of laplacian.jl:60-75 (CHOLMOD factors any M x P).
+// ------------------------------------------------------------------------------------
+constexpr int SPL_T = 512;        // row-transform threads (256 VGPRs: a radix-13 butterfly + its roots)
+constexpr int SPL_MMAX = 8192;    // one LDS buffer of M complex (128 KB)
+constexpr int SPL_KT = 256;       // recurrence kernels: wavenumbers per workgroup
+
+// One decimation-in-frequency stage of radix R, in place: butterfly (block b, n) reads the R
+// values n + m span of its block, does the R-point DFT, multiplies output q by W_Ls^(n q)
+// (Ls = R span, the stage's sub-transform length) and writes it back to n + q span.  Every
+// butterfly writes only the slots it read, so one barrier per stage and one butterfly's values
+// in registers.  After all stages frequency k sits at perm[k] (mixed-radix digit reversal).
+template <int R, bool INV>
+__device__ void spl_stage(double2 *buf, const double2 *__restrict__ tw, int M, int span) {
+    const int Ls = R * span, sc = M / Ls;  // W_Ls^e = tw[e sc]
+    const int rstep = M / R;               // W_R^e = tw[e rstep]
+    double2 wr[R];
+    if constexpr (R != 2 && R != 4 && R != 8) {
+#pragma unroll
+        for (int e = 0; e < R; ++e) {
+            wr[e] = tw[e * rstep];
+            if (INV) wr[e].y = -wr[e].y;
+        }
+    }
+    for (int b = threadIdx.x; b < M / R; b += SPL_T) {
+        const int blk = b / span, n = b - blk * span;
+        double2 *x = buf + (size_t)blk * Ls + n;
+        double2 v[R];
+#pragma unroll
+        for (int m = 0; m < R; ++m) v[m] = x[m * span];
+        if constexpr (R == 8) dft8<INV>(v);
+        else if constexpr (R == 4) dft4<INV>(v[0], v[1], v[2], v[3]);
+        else if constexpr (R == 2) dft2<INV>(v[0], v[1]);
+        else {  // odd prime radix: direct R-point DFT
+            double2 o[R];
+#pragma unroll
+            for (int q = 0; q < R; ++q) {
+                double2 acc = v[0];
+                int e = 0;
+#pragma unroll
+                for (int m = 1; m < R; ++m) {
+                    e += q;
+                    if (e >= R) e -= R;
+                    acc = cadd(acc, cmul(v[m], wr[e]));
+                }
+                o[q] = acc;
+            }
+#pragma unroll
+            for (int q = 0; q < R; ++q) v[q] = o[q];
+        }
+        x[0] = v[0];
+        int e = 0;  // n q sc mod M
+        const int step = n * sc;
+#pragma unroll
+        for (int q = 1; q < R; ++q) {
+            e += step;
+            if (e >= M) e -= M;
+            double2 w = tw[e];
+            if (INV) w.y = -w.y;
+            x[q * span] = span > 1 ? cmul(v[q], w) : v[q];
+        }
+    }
+    __syncthreads();
+}
+
+// the whole row transform in place (input synchronised in buf, natural order).  Planned rows:
+// result synchronised in buf with frequency k at a.perm[k]; direct DFT: natural order.
+template <bool INV>
+__device__ void spl_fft(double2 *buf, const SpecArgs &a, int M) {
+    if (a.nrad == 0) {  // direct DFT: outputs to registers, then back in place
+        constexpr int OUT = SPL_MMAX / SPL_T;
+        double2 o[OUT];
+#pragma unroll
+        for (int q = 0; q < OUT; ++q) {
+            const int k = threadIdx.x + q * SPL_T;
+            if (k < M) o[q] = dft_at<INV>(buf, a.tw, M, k);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < OUT; ++q) {
+            const int k = threadIdx.x + q * SPL_T;
+            if (k < M) buf[k] = o[q];
+        }
+        __syncthreads();
+        return;
+    }
+    int span = M;
+    for (int p = 0; p < a.nrad; ++p) {
+        const int R = a.rad[p];
+        span /= R;
+        switch (R) {
+            case 2: spl_stage<2, INV>(buf, a.tw, M, span); break;
+            case 3: spl_stage<3, INV>(buf, a.tw, M, span); break;
+            case 4: spl_stage<4, INV>(buf, a.tw, M, span); break;
+            case 5: spl_stage<5, INV>(buf, a.tw, M, span); break;
+            case 7: spl_stage<7, INV>(buf, a.tw, M, span); break;
+            case 8: spl_stage<8, INV>(buf, a.tw, M, span); break;
+            case 11: spl_stage<11, INV>(buf, a.tw, M, span); break;
+            default: spl_stage<13, INV>(buf, a.tw, M, span); break;
+        }
+    }
+}
+
+template <class S, bool INV>
+__global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
+    using US = typename Store<S>::C;
+    const int M = (int)a.M, NH = M / 2, t = threadIdx.x;
+    const bool odd = M & 1;
+    const int KC = odd ? NH + 1 : NH;  // (see spec_passA_gen)
+    const int KS = a.KS;
+    const int64_t Pl = a.P, ld = a.ld;
+    extern __shared__ double2 buf[];
+    __shared__ double pinw[SPL_T / 64];
+    double pin = 0;
+    if constexpr (INV) {
+        const double pinp = a.pinned0 ? pin_part<SPL_T>(a, t) : 0.0;
+        pin = pin_total<SPL_T>(pinp, pinw);
+        if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
+    }
+    for (int64_t j = blockIdx.x; j < Pl; j += gridDim.x) {
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
+        if constexpr (!INV) {
+            const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
+            const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
+            const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
+            for (int i = t; i < M; i += SPL_T) {
+                const double z1 = r1[i], z2 = r2[i];
+                buf[i] = make_double2(p0 * z1 + p1 * z2, p2 * z1 + p3 * z2);
+            }
+            __syncthreads();
+            spl_fft<false>(buf, a, M);
+            auto Z = [&](int k) { return buf[a.nrad ? a.perm[k] : k]; };
+            for (int k = t; k < KC; k += SPL_T) {
+                const double2 Zk = Z(k);
+                if (k == 0) {  // real lines k = 0 (and k = M/2 for even M)
+                    Urow[0] = Store<S>::c(make_double2(Zk.x, 0));
+                    Urow[KS] = Store<S>::c(make_double2(Zk.y, 0));
+                    if (!odd) {
+                        const double2 Zn = Z(NH);
+                        Urow[NH] = Store<S>::c(make_double2(Zn.x, 0));
+                        Urow[KS + NH] = Store<S>::c(make_double2(Zn.y, 0));
+                    }
+                } else {
+                    const double2 Zm = Z(M - k);
+                    Urow[k] = Store<S>::c(make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5));
+                    Urow[KS + k] = Store<S>::c(make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5));
+                }
+            }
+            __syncthreads();  // the next row overwrites buf
+        } else {
+            for (int k = t; k < KC; k += SPL_T) {
+                if (k == 0) {
+                    buf[0] = make_double2(d2(Urow[0]).x, d2(Urow[KS]).x);
+                    if (!odd) buf[NH] = make_double2(d2(Urow[NH]).x, d2(Urow[KS + NH]).x);
+                } else {
+                    const double2 X0 = d2(Urow[k]), X1 = d2(Urow[KS + k]);
+                    buf[k] = make_double2(X0.x - X1.y, X0.y + X1.x);
+                    buf[M - k] = make_double2(X0.x + X1.y, X1.x - X0.y);
+                }
+            }
+            __syncthreads();
+            spl_fft<true>(buf, a, M);
+            S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
+            S *row1 = out1 + (size_t)(j + 1) * ld;
+            const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
+            S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
+            S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
+            S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
+            for (int i = t; i < M; i += SPL_T) {
+                const double2 z = buf[a.nrad ? a.perm[i] : i];
+                const double x1 = (pin_row && i == 0) ? 0.0 : z.x - pin, x2 = z.y;
+                store_row_with_ghosts(row1, grow1, M, i, (S)(a.pin_out[0] * x1 + a.pin_out[1] * x2));
+                if (row2) store_row_with_ghosts(row2, grow2, M, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
+            }
+            __syncthreads();  // the next row overwrites buf
+        }
+    }
+}
+
+// lines k of (chunk blockIdx.x): the generic pass A's backward filter and summaries
+template <class S>
+__global__ __launch_bounds__(SPL_KT) void spec_passA_split(SpecArgs a) {
+    using US = typename Store<S>::C;
+    const int c = blockIdx.x, k = blockIdx.y * SPL_KT + threadIdx.x;
+    if (k >= a.KH) return;
+    const int KS = a.KS, s0 = c * a.L, e = s0 + a.L - 1;
+    double2 u[2] = {make_double2(0, 0), make_double2(0, 0)}, bw[2] = {u[0], u[1]};
+    double2 rr[2];
+    double cs[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        rr[s] = a.crr[s * KS + k];
+        cs[s] = a.ccs[s * KS + k];
+    }
+    double dc = 0;
+    for (int j = e; j >= s0; --j) {
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const double2 B = d2(Urow[s * KS + k]);
+            if (s == 0 && k == 0) {
+                dc += B.x;
+                a.hline[j] = B.x;
+            }
+            u[s] = cfma(rr[s].x, u[s], cscale(B, cs[s]));
+            Urow[s * KS + k] = Store<S>::c(u[s]);
+            bw[s] = cfma(rr[s].y, bw[s], u[s]);
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const size_t o = ((size_t)c * 2 + s) * KS + k;
+        a.ULS[o] = u[s];
+        a.WLS[o] = cscale(bw[s], a.coef[s * KS + k].qm1);
+    }
+    if (k == 0) a.dcpart[c] = dc;
+}
+
+// lines k of (chunk blockIdx.x): carries, the generic pass B's forward filter, X in place
+template <class S>
+__global__ __launch_bounds__(SPL_KT) void spec_passB_split(SpecArgs a) {
+    using US = typename Store<S>::C;
+    const int c = blockIdx.x, k = blockIdx.y * SPL_KT + threadIdx.x;
+    if (k >= a.KH) return;
+    const int KS = a.KS, L = a.L, s0 = c * L, e = s0 + L - 1;
+    const double delta = a.scal[0];
+    const bool inject = a.pinned0 && a.rank == 0;
+    const bool sing = a.pinned0 && k == 0;  // (s = 0, k = 0): the singular line, from a.line
+    const double line0 = a.scal[2], line1 = a.scal[3];
+    double2 cu[2], w[2], rr[2];
+    double cs[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        cu[s] = w[s] = make_double2(0, 0);
+        if (!(s == 0 && sing)) chunk_carry(a, s, k, c, delta, inject, cu[s], w[s]);
+        rr[s] = a.crr[s * KS + k];
+        cs[s] = a.ccs[s * KS + k];
+    }
+    for (int j = s0; j <= e; ++j) {
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            double2 ul = d2(Urow[s * KS + k]);
+            if (s == 0 && inject && j == 0) ul.x += cs[s] * delta;  // Poisson compatibility shift
+            w[s] = cfma(rr[s].x, w[s], cadd(ul, cu[s]));
+            cu[s] = cscale(cu[s], rr[s].y);
+            const double2 X = (s == 0 && sing) ? make_double2((line0 + (double)j * line1) + a.line[j], 0) : w[s];
+            Urow[s * KS + k] = Store<S>::c(X);
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
 template <int N, class S>
@@ -1565,7 +1835,33 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
         case 8192: return a.f32 ? launch_half_t<float>(passB, a, s) : launch_half_t<double>(passB, a, s);
         default: break;
     }
-    if (a.M > GEN_MMAX) return QG_ERR_UNSUPPORTED;
+    // (QG_SPLIT_FORCE: tests run generic-size rows through the split passes)
+    if (a.M > GEN_MMAX || std::getenv("QG_SPLIT_FORCE") != nullptr) {
+        if (a.M > SPL_MMAX) return QG_ERR_UNSUPPORTED;
+        const size_t lds = sizeof(double2) * (size_t)a.M;
+        const unsigned rows = (unsigned)std::min<int64_t>(a.P, 1024);
+        const dim3 rgrid((unsigned)a.Nc, (unsigned)((a.KH + SPL_KT - 1) / SPL_KT));
+        auto fft = [&](const void *fn, auto kernel) -> int {
+            QG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            kernel<<<rows, SPL_T, lds, s>>>(a);
+            QG_LAUNCH_CHECK();
+            return QG_OK;
+        };
+        if (!passB) {
+            QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, false>, spec_fft_split<float, false>)
+                           : fft((const void *)spec_fft_split<double, false>, spec_fft_split<double, false>));
+            if (a.f32) spec_passA_split<float><<<rgrid, SPL_KT, 0, s>>>(a);
+            else spec_passA_split<double><<<rgrid, SPL_KT, 0, s>>>(a);
+            QG_LAUNCH_CHECK();
+        } else {
+            if (a.f32) spec_passB_split<float><<<rgrid, SPL_KT, 0, s>>>(a);
+            else spec_passB_split<double><<<rgrid, SPL_KT, 0, s>>>(a);
+            QG_LAUNCH_CHECK();
+            QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, true>, spec_fft_split<float, true>)
+                           : fft((const void *)spec_fft_split<double, true>, spec_fft_split<double, true>));
+        }
+        return QG_OK;
+    }
     const size_t lds = sizeof(double2) * 3 * (size_t)a.M;  // row, transform, twiddles
     auto go = [&](const void *fn, auto kernel) -> int {
         QG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1583,11 +1879,12 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
     return QG_OK;
 }
 
-// power-of-two rows 8 .. 8192 (FFT passes), or any other rows 3 .. GEN_MMAX (generic passes)
+// power-of-two rows 8 .. 8192 (FFT passes), any other rows 3 .. GEN_MMAX (generic passes)
+// and GEN_MMAX .. SPL_MMAX (split passes)
 bool SpectralSolver::supports(int64_t M, int64_t P) {
     if (P < 2) return false;
     if (M >= 8 && M <= 8192 && (M & (M - 1)) == 0) return true;
-    return M >= 3 && M <= GEN_MMAX;
+    return M >= 3 && M <= SPL_MMAX;
 }
 
 // Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic; 32 for
@@ -1700,8 +1997,10 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     const bool wide = M == 2 * HN;  // wide-row passes: half-length twiddles + system-0 rows
     const size_t n_tw2 = wide ? align_up(sizeof(double2) * HN) : 0;
     const size_t n_half = wide ? align_up((f32 ? sizeof(float) : sizeof(double)) * (size_t)P * M) : 0;
+    // split passes with a plan: where the DIF stages leave frequency k (digit reversal)
+    const size_t n_perm = a.nrad > 0 ? align_up(sizeof(int) * M) : 0;
     bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart +
-             n_tw2 + n_half;
+             n_tw2 + n_half + n_perm;
     if (hipMalloc(&mem_, bytes_) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -1728,6 +2027,22 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.pinpart = (double *)take(n_pinpart);
     a.tw2 = wide ? (const double2 *)take(n_tw2) : nullptr;
     a.half_tmp = wide ? (void *)take(n_half) : nullptr;
+    a.perm = nullptr;
+    if (a.nrad > 0) {
+        int *d_perm = (int *)take(n_perm);
+        std::vector<int> perm(M);
+        for (int64_t k = 0; k < M; ++k) {
+            int64_t rem = k, span = M, pos = 0;
+            for (int q = 0; q < a.nrad; ++q) {
+                span /= a.rad[q];
+                pos += (rem % a.rad[q]) * span;
+                rem /= a.rad[q];
+            }
+            perm[k] = (int)pos;
+        }
+        QG_HIP(hipMemcpy(d_perm, perm.data(), sizeof(int) * M, hipMemcpyHostToDevice));
+        a.perm = d_perm;
+    }
     a.tw = d_tw;
     a.coef = d_coef;
     QG_HIP(hipMemcpy(d_tw, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice));

@@ -69,6 +69,7 @@ struct SpecArgs {
     const double2 *tw2;       // wide rows (M = 8192): M/2 twiddles of the half-length FFT
     void *half_tmp;           // wide rows: [P][M] system-0 result, state precision (pass B 0 -> 1)
     int nrad, rad[16];        // generic rows: mixed-radix pass plan (0 = direct DFT)
+    const int *perm;          // split rows with a plan: position of frequency k after the DIF stages
     int fuse_pin;             // one rank, no transport: spec_carry also does spec_pin's work
     int npin;                 // pin parts pass B sums (pinpart[0 .. npin))
 };

@@ -74,15 +74,58 @@ def test_reference_benchmark_sweep_sizes(env, M):
 
 def test_generic_rows_wide(env):
     """Wide generic rows on rectangular slabs: M = 2000 and 3000 (mixed-radix passes), 1999
-    (prime: direct DFT); M above the generic limit (3200) refused."""
+    (prime: direct DFT); non-power-of-two M above the split limit (8192) refused."""
     qg, O, R = env
     for M in (2000, 1999, 3000):
         st = qg.run_model_no_output(qg.bench_model(M, P=24, dt=600.0), nsteps=3)
         ref = O.State(R.bench_model(M, P=24, dt=600.0)).run(3)
         assert rel(st.to_numpy("psi"), ref.psi) < TOL, M
     with pytest.raises(qg.QGError) as e:
-        qg.State(qg.bench_model(4000, P=8))
+        qg.State(qg.bench_model(8200, P=8))
     assert e.value.status == -2
+
+
+@pytest.mark.parametrize("M,P,steps", [(3328, 32, 3), (5000, 32, 3), (6000, 24, 3), (8191, 16, 2), (4001, 20, 2)])
+def test_split_rows_beyond_generic(env, M, P, steps):
+    """Non-power-of-two rows wider than the generic passes (3200 < M <= 8192): the split
+    passes -- row DFT in place in one LDS buffer (mixed-radix DIF: 3328 = 8 8 4 13,
+    5000 = 8 5^4, 6000 = 8 2 3 5^3; direct DFT: 8191 and 4001 are prime), recurrences one
+    thread per wavenumber.  The reference factors any M x P (laplacian.jl:60-75)."""
+    qg, O, R = env
+    st = qg.run_model_no_output(qg.bench_model(M, P=P, dt=600.0), nsteps=steps)
+    ref = O.State(R.bench_model(M, P=P, dt=600.0)).run(steps)
+    for n in ("psi", "zeta"):
+        assert rel(st.to_numpy(n), getattr(ref, n)) < TOL, (n, M)
+    if M == 5000:  # PCG with the split solve as its preconditioner
+        pc = qg.run_model_no_output(qg.bench_model(M, P=P, dt=600.0), nsteps=steps, solver=1)
+        assert rel(pc.to_numpy("psi"), ref.psi) < TOL
+
+
+@pytest.mark.parametrize("M,P", [(3000, 24), (1001, 16), (45, 40), (120, 16), (2310, 12)])
+def test_split_passes_match_generic(env, M, P, monkeypatch):
+    """QG_SPLIT_FORCE routes generic-size rows through the split passes: same answer as the
+    generic passes (different FFT order: roundoff only) and the oracle."""
+    qg, O, R = env
+    m = qg.bench_model(M, P=P, dt=600.0)
+    gen = qg.run_model_no_output(m, nsteps=4)
+    monkeypatch.setenv("QG_SPLIT_FORCE", "1")
+    spl = qg.run_model_no_output(m, nsteps=4)
+    ref = O.State(R.bench_model(M, P=P, dt=600.0)).run(4)
+    for n in ("psi", "zeta", "f_store"):
+        err = rel(spl.to_numpy(n), gen.to_numpy(n))
+        # (3000 x 24: the wide, short slab amplifies the two FFT orders' roundoff: 3.8e-12)
+        assert err < 2e-11, (n, err)
+    assert rel(spl.to_numpy("psi"), ref.psi) < TOL
+
+
+def test_split_rows_f32(env):
+    """F32 state through the split passes (M = 5000): psi within the F32 bar of the F64 run."""
+    import torch
+    qg, O, R = env
+    m = qg.bench_model(5000, P=32, dt=600.0)
+    a = qg.run_model_no_output(m, nsteps=3)
+    b = qg.run_model_no_output(m, nsteps=3, dtype=torch.float32)
+    assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 5e-3
 
 
 def test_invalid_arguments_are_refused(env):
