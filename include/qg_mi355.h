@@ -142,6 +142,20 @@ int qg_slot(const qg_ctx *ctx, int which, int logical, int *physical);
 int qg_set_slots(qg_ctx *ctx, const int heads[3]); /* restore a saved rotation (resume)  */
 int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2,3       */
 int qg_get_stats(qg_ctx *ctx, qg_stats *out);
+/* PCG with the spectral preconditioner and an invertible P_fwd (the default) takes the
+ * certified step: psi = the spectral solve, accepted when the 5-point residual satisfies
+ * ||b - B x|| <= pcg_rtol ||b|| (PCG's first iteration with alpha = 1).  Default: DEFERRED --
+ * the residual check runs on the device (on one rank fused into the next step's tendency,
+ * which reads exactly that solve's zeta and psi; else as its own pass after the solve) and
+ * its verdict is latched there: no host round trip, qg_run can replay PCG steps as HIP graphs.
+ * A failed certification is reported by the next qg_synchronize (QG_ERR_NOT_CONVERGED) and
+ * by qg_pcg_certificate.  sync = 1 (or QG_PCG_SYNC=1 at create): the host reads every
+ * residual and runs the general PCG iteration when the certificate fails (the old form).  */
+int qg_set_pcg_sync(qg_ctx *ctx, int sync);
+/* deferred certificates so far: solves certified, failures, first failing solve (1-based,
+ * 0 = none), worst relative residual.  QG_ERR_UNSUPPORTED without the PCG solver.       */
+int qg_pcg_certificate(qg_ctx *ctx, int64_t *solves, int64_t *failures, int64_t *first_failure,
+                       double *worst_relres);
 /* the same, flattened (no struct): PCG iterations and relative residuals of the last solve */
 int qg_solver_stats(qg_ctx *ctx, int *it_poisson, int *it_helm, double *relres_p, double *relres_h);
 int qg_synchronize(qg_ctx *ctx);

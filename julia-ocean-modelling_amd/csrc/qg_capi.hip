@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 #include <memory>
 #include <new>
@@ -87,6 +88,8 @@ struct qg_ctx {
     std::unique_ptr<SpectralSolver> spec;
     std::unique_ptr<PcgSolver> pcg;
     int last_status = QG_OK;  // of the last solve (PCG: QG_ERR_NOT_CONVERGED is kept here)
+    int pcg_sync = -1;        // qg_set_pcg_sync (-1: the environment's / the default)
+    int64_t cert_reported = 0;  // deferred PCG certification failures already reported
     size_t F = 0;  // doubles per (M+2, P+2) field
 
     void *fieldv(void *base, int layer, int slot) const {
@@ -174,7 +177,12 @@ static int build_solver(qg_ctx *c) {
         auto s = std::make_unique<PcgSolver>();
         QG_CHECK(s->init(p.M, p.P, p.P * c->nranks, c->rank, c->nranks, p.dx, alpha, 1, c->d.Pinv, p.P_fwd,
                          p.precond, p.pcg_rtol, p.pcg_maxit, p.chunk_rows));
+        // deferred certification: fused into the next tendency on one rank (no transport)
+        s->set_fuse(!c->distributed);
+        if (c->pcg_sync >= 0) s->set_deferred(c->pcg_sync == 0);
+        QG_CHECK(s->reset_latch(c->stream));
         c->pcg = std::move(s);
+        c->cert_reported = 0;
         return QG_OK;
     }
     if (!SpectralSolver::supports(p.M, p.P)) return QG_ERR_UNSUPPORTED;
@@ -350,7 +358,19 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
             fill_wrap_rows(c, a.zeta[l], a.zeta_rows[l]);
             fill_wrap_rows(c, a.psi[l], a.psi_rows[l]);
         }
-        QG_CHECK(launch_tendency(a, c->stream));
+        bool done = false;
+        if constexpr (std::is_same<T, double>::value) {
+            // the previous solve's deferred PCG certification rides in this tendency (it reads
+            // exactly that solve's zeta and psi)
+            if (c->pcg && c->pcg->pending()) {
+                c->pcg->fill_cert_args(a);
+                int nblk = 0;
+                QG_CHECK(launch_tendency_cert(a, &nblk, c->stream));
+                QG_CHECK(c->pcg->latch_fused(nblk, c->stream));
+                done = true;
+            }
+        }
+        if (!done) QG_CHECK(launch_tendency(a, c->stream));
     } else {
         // halo rows of psi (depth 2; zeta uses the inner two) from the neighbouring slabs,
         // grouped with the pending ghost-row refresh of the previous step's outputs
@@ -465,7 +485,8 @@ int qg_step(qg_ctx *c, int64_t timestep) {
 // tools/graph_bench.py), so stream launches are the default.
 static bool graphs_enabled(const qg_ctx *c) {
     const char *e = std::getenv("QG_GRAPH");
-    return e && std::atoi(e) != 0 && c->graph_ok && !c->distributed && c->spec && !c->pcg;
+    // (PCG: only the deferred form, which never reads the residual on the host)
+    return e && std::atoi(e) != 0 && c->graph_ok && !c->distributed && (c->spec || (c->pcg && c->pcg->deferred()));
 }
 
 // the graph of three AB3 steps starting from the current slot rotation (captured on first use)
@@ -562,6 +583,15 @@ int qg_get_stats(qg_ctx *c, qg_stats *out) {
         out->iters[0] = out->iters[1] = c->pcg->iterations();
         out->relres[0] = c->pcg->relres(0);
         out->relres[1] = c->pcg->relres(1);
+        if (c->pcg->deferred()) {  // the last certified solve's residuals, from the latch
+            double lt[8];
+            QG_HIP(hipSetDevice(c->device));
+            QG_CHECK(c->pcg->certify_pending(c->stream, c->distributed ? comm_allgather : nullptr, c->comm));
+            QG_HIP(hipMemcpyAsync(lt, c->pcg->latch(), sizeof(lt), hipMemcpyDeviceToHost, c->stream));
+            QG_CHECK(ctx_wait(c, "qg_get_stats"));
+            out->relres[0] = lt[4];
+            out->relres[1] = lt[5];
+        }
         return QG_OK;
     }
     if (!c->spec) return QG_OK;
@@ -681,7 +711,44 @@ int qg_synchronize(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     QG_HIP(hipSetDevice(c->device));
     QG_CHECK(flush_ghosts(c));
+    if (c->pcg && c->pcg->deferred()) {  // deferred PCG: new certification failures?
+        QG_CHECK(c->pcg->certify_pending(c->stream, c->distributed ? comm_allgather : nullptr, c->comm));
+        double lt[8];
+        QG_HIP(hipMemcpyAsync(lt, c->pcg->latch(), sizeof(lt), hipMemcpyDeviceToHost, c->stream));
+        QG_CHECK(ctx_wait(c, "qg_synchronize"));
+        if ((int64_t)lt[1] > c->cert_reported) {
+            c->cert_reported = (int64_t)lt[1];
+            return QG_ERR_NOT_CONVERGED;
+        }
+        return QG_OK;
+    }
     return ctx_wait(c, "qg_synchronize");
+}
+
+int qg_set_pcg_sync(qg_ctx *c, int sync) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    c->pcg_sync = sync != 0 ? 1 : 0;
+    if (c->pcg) {
+        QG_HIP(hipSetDevice(c->device));
+        QG_CHECK(c->pcg->certify_pending(c->stream, c->distributed ? comm_allgather : nullptr, c->comm));
+        c->pcg->set_deferred(sync == 0);
+    }
+    return QG_OK;
+}
+
+int qg_pcg_certificate(qg_ctx *c, int64_t *solves, int64_t *failures, int64_t *first_failure, double *worst_relres) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    if (!c->pcg) return QG_ERR_UNSUPPORTED;
+    QG_HIP(hipSetDevice(c->device));
+    QG_CHECK(c->pcg->certify_pending(c->stream, c->distributed ? comm_allgather : nullptr, c->comm));
+    double lt[8];
+    QG_HIP(hipMemcpyAsync(lt, c->pcg->latch(), sizeof(lt), hipMemcpyDeviceToHost, c->stream));
+    QG_CHECK(ctx_wait(c, "qg_pcg_certificate"));
+    if (solves) *solves = (int64_t)lt[0];
+    if (failures) *failures = (int64_t)lt[1];
+    if (first_failure) *first_failure = (int64_t)lt[2];
+    if (worst_relres) *worst_relres = lt[3];
+    return QG_OK;
 }
 
 // ---- multi-GPU -------------------------------------------------------------------------
@@ -763,6 +830,7 @@ int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], con
         // CG on -A with b = -(proj_in f): the same x as A x = proj_in f
         s->pcg = std::make_unique<PcgSolver>();
         st = s->pcg->init(M, P, P, 0, 1, dx, alpha, pinned[0], proj_in, proj_out, precond, 1e-13, 4000, 0);
+        s->pcg->set_deferred(false);  // a factor handle's solve returns its own verdict
     } else {
         st = s->spec.init(M, P, P, 0, 1, dx, alpha, pinned[0], proj_in, proj_out, 0);
     }

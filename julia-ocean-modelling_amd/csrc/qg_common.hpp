@@ -192,6 +192,13 @@ struct TendArgsT {
     RowSrcT<T> zeta_rows[2];
     RowSrcT<T> psi_rows[2];
     const double *wind;        // [P] upper-layer wind forcing per local row, or nullptr (off)
+    // PCG certification fused into the next tendency (launch_tendency_cert, F64, one rank):
+    // per workgroup (b,b), (r,r) of both systems for the solve that produced psi from zeta
+    double *cert;              // [workgroups][4] partials
+    double cert_in[4];         // proj_in (b_s = -(proj_in zeta)_s)
+    double cert_pinv[4];       // P_fwd^-1 (psi~ = P_fwd^-1 psi)
+    double cert_alpha[2];      // construct_spA shifts
+    int cert_pin;              // system 0 pinned at interior (0, 0)
 };
 using TendArgs = TendArgsT<double>;
 
@@ -204,6 +211,9 @@ inline double wind_row(double tau0, double rho0, double H1, double dx, int64_t P
 
 int launch_tendency(const TendArgsT<double> &a, hipStream_t s);
 int launch_tendency(const TendArgsT<float> &a, hipStream_t s);
+// the same tendency, both layers per workgroup, also certifying the previous solve (a.cert):
+// *nblk = workgroups launched (partials written)
+int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s);
 int launch_laplace(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
 int launch_cd(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
 int launch_arakawa(const double *z, const double *p, double *out, int64_t M, int64_t P, double dx,

@@ -374,6 +374,56 @@ __global__ void pcg_scalar(PcgArgs a, int what, const double *gathered, int nran
     }
 }
 
+// ---- deferred certification: verdict latched on the device ------------------------------
+__device__ void cert_latch(PcgArgs a, double *latch, double rtol, const double bb[2], const double rr[2]) {
+    double worst = 0;
+    for (int s = 0; s < 2; ++s) {
+        const double rel = bb[s] > 0 ? sqrt(rr[s] / bb[s]) : sqrt(rr[s]);
+        a.scal[PCG_BB + s] = bb[s];
+        a.scal[PCG_RR + s] = rr[s];
+        latch[4 + s] = rel;
+        worst = (rel != rel || rel > worst) ? rel : worst;  // NaN sticks
+    }
+    const double n = latch[0] + 1;
+    latch[0] = n;
+    if (!(worst <= rtol)) {
+        if (latch[1] == 0) latch[2] = n;
+        latch[1] += 1;
+    }
+    const double w = latch[3];
+    latch[3] = (worst != worst || w != w) ? (worst + w) : (worst > w ? worst : w);
+}
+
+// from the check pass's scalars (pcg_fast_scalar what 2)
+__global__ void pcg_cert_latch_scal(PcgArgs a, double *latch, double rtol) {
+    if (threadIdx.x != 0) return;
+    const double bb[2] = {a.scal[PCG_BB], a.scal[PCG_BB + 1]}, rr[2] = {a.scal[PCG_RR], a.scal[PCG_RR + 1]};
+    cert_latch(a, latch, rtol, bb, rr);
+}
+
+// from the certifying tendency's partials (fixed order)
+__global__ __launch_bounds__(1024) void pcg_cert_latch_part(PcgArgs a, const double *part, int nblk, double *latch,
+                                                            double rtol) {
+    __shared__ double sm[4][1024];
+    double t[4] = {0, 0, 0, 0};
+    for (int b = threadIdx.x; b < nblk; b += 1024)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[k] += part[4 * (size_t)b + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sm[k][threadIdx.x] = t[k];
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+        if (threadIdx.x < o)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) sm[k][threadIdx.x] += sm[k][threadIdx.x + o];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const double bb[2] = {sm[0][0], sm[2][0]}, rr[2] = {sm[1][0], sm[3][0]};
+        cert_latch(a, latch, rtol, bb, rr);
+    }
+}
+
 // ------------------------------------------------------------------------------------
 int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks, double dx, const double alpha[2],
                     int pinned0, const double proj_in[4], const double proj_out[4], int precond, double rtol,
@@ -417,7 +467,10 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
     }
     const size_t F = (size_t)(M + 2) * (size_t)(P + 2);
     nblk_ = (int)(((M + PCG_T - 1) / PCG_T) * std::min<int64_t>(P, PCG_ROWB));
-    const size_t bytes = sizeof(double) * (10 * F + 6 * (size_t)nblk_ + 64 + 6 * (size_t)nranks);
+    // certifying tendency: at most one workgroup per 256 columns and 4 rows
+    cert_part_n_ = ((M + 255) / 256) * std::max<int64_t>(1, (P + 3) / 4);
+    const size_t bytes = sizeof(double) * (10 * F + 6 * (size_t)nblk_ + 64 + 6 * (size_t)nranks + 8 +
+                                           4 * (size_t)cert_part_n_);
     if (hipMalloc(&mem_, bytes) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -434,6 +487,9 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
     a.partial = m + 10 * F;
     a.scal = a.partial + 6 * (size_t)nblk_;
     gathered_ = a.scal + 64;
+    latch_ = gathered_ + 6 * (size_t)nranks;
+    cert_part_ = latch_ + 8;
+    if (const char *e = std::getenv("QG_PCG_SYNC")) deferred_ = std::atoi(e) == 0;
     return QG_OK;
 }
 
@@ -472,6 +528,41 @@ static int reduce_fast(PcgArgs &a, int nblk, int what, double *gathered, hipStre
     return QG_OK;
 }
 
+void PcgSolver::fill_cert_args(TendArgsT<double> &t) const {
+    t.cert = cert_part_;
+    std::memcpy(t.cert_in, a_.proj_in, sizeof(t.cert_in));
+    std::memcpy(t.cert_pinv, a_.pinv_out, sizeof(t.cert_pinv));
+    t.cert_alpha[0] = a_.alpha[0];
+    t.cert_alpha[1] = a_.alpha[1];
+    t.cert_pin = (a_.pinned0 && a_.rank == 0) ? 1 : 0;
+}
+
+int PcgSolver::latch_fused(int nblk, hipStream_t s) {
+    if (nblk > cert_part_n_) return QG_ERR_INVALID_ARG;
+    pcg_cert_latch_part<<<1, 1024, 0, s>>>(a_, cert_part_, nblk, latch_, rtol_);
+    QG_LAUNCH_CHECK();
+    pending_ = false;
+    return QG_OK;
+}
+
+int PcgSolver::certify_pending(hipStream_t s, SpectralSolver::GatherFn gather, void *user) {
+    if (!pending_) return QG_OK;
+    // prev_: the arguments (inputs, outputs) of the solve being certified
+    const dim3 grid((unsigned)((prev_.M + PCG_T - 1) / PCG_T), (unsigned)std::min<int64_t>(prev_.P, PCG_ROWB));
+    pcg_cert_check<<<grid, PCG_T, 0, s>>>(prev_);
+    QG_LAUNCH_CHECK();
+    QG_CHECK(reduce_fast<4>(prev_, nblk_, 2, gathered_, s, gather, user));
+    pcg_cert_latch_scal<<<1, 64, 0, s>>>(prev_, latch_, rtol_);
+    QG_LAUNCH_CHECK();
+    pending_ = false;
+    return QG_OK;
+}
+
+int PcgSolver::reset_latch(hipStream_t s) {
+    QG_HIP(hipMemsetAsync(latch_, 0, sizeof(double) * 8, s));
+    return QG_OK;
+}
+
 int PcgSolver::solve(const double *in1, const double *in2, double *out1, double *out2, int ghost_rows,
                      hipStream_t s, SpectralSolver::GatherFn gather, void *user, HaloFn halo, void *halo_user) {
     if (!mem_) return QG_ERR_NOT_BOUND;
@@ -505,6 +596,22 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
     int status = QG_ERR_NOT_CONVERGED;
     bool resume = false;  // continue the general loop after a fast first iteration
     int first_it = 1;
+    if (deferred() && out2) {
+        // deferred: the spectral solve, then the check on the device -- in the next tendency
+        // (fuse_) or right here -- with the verdict latched (latch_); no host round trip
+        // a previous solve's fused check that never got its tendency runs first
+        QG_CHECK(certify_pending(s, gather, user));
+        QG_CHECK(pre_.solve(a.in1, a.in2, a.out1, a.out2, ghost_rows, s, gather, user, a.proj_in, a.proj_out));
+        if (!ghost_rows && halo) {
+            double *f[2] = {a.out1, a.out2};
+            QG_CHECK(halo(halo_user, f, 2, a.M, a.P, -1, nullptr, s));
+        }
+        iters_ = 1;
+        prev_ = a;
+        pending_ = true;
+        if (!fuse_) QG_CHECK(certify_pending(s, gather, user));
+        return QG_OK;
+    }
     if (precond_ == QG_PRECOND_SPECTRAL && cert_ && out2) {
         // psi = P_fwd z0 straight from the spectral solve, then one certification pass
         QG_CHECK(pre_.solve(a.in1, a.in2, a.out1, a.out2, ghost_rows, s, gather, user, a.proj_in, a.proj_out));

@@ -40,6 +40,25 @@ public:
     int iterations() const { return iters_; }
     double relres(int s) const { return relres_[s]; }
 
+    // ---- deferred certification (default; QG_PCG_SYNC=1 or qg_set_pcg_sync restores the
+    // host-checked iteration).  The certified step's residual check runs on the device and
+    // its verdict is latched there (no host round trip, graph-capturable): fused into the
+    // next tendency when `fuse` (one rank), else as its own pass right after the solve.
+    void set_deferred(bool on) { deferred_ = on; }
+    bool deferred() const { return deferred_ && cert_ && precond_ == QG_PRECOND_SPECTRAL; }
+    void set_fuse(bool on) { fuse_ = on; }
+    bool pending() const { return pending_; }
+    // the certification fields of the next tendency's arguments
+    void fill_cert_args(TendArgsT<double> &t) const;
+    // after launch_tendency_cert: fold its nblk partials and latch the verdict
+    int latch_fused(int nblk, hipStream_t s);
+    // a pending fused certification with no tendency coming: run the check pass now
+    int certify_pending(hipStream_t s, SpectralSolver::GatherFn gather = nullptr, void *user = nullptr);
+    // latch record (device, doubles): [0] solves certified, [1] failures, [2] first failing
+    // solve (1-based, 0 = none), [3] worst relres, [4] [5] last relres (Poisson, Helmholtz)
+    const double *latch() const { return latch_; }
+    int reset_latch(hipStream_t s);
+
 private:
     int reduce(int what, hipStream_t s, SpectralSolver::GatherFn gather, void *user);
     PcgArgs a_{};
@@ -49,6 +68,11 @@ private:
     double rtol_ = 1e-13, relres_[2] = {-1, -1};
     void *mem_ = nullptr;
     double *gathered_ = nullptr;
+    bool deferred_ = true, fuse_ = false, pending_ = false;
+    PcgArgs prev_{};               // the last deferred solve's arguments (its pending check)
+    double *latch_ = nullptr;      // [8]
+    double *cert_part_ = nullptr;  // [workgroups][4] of the certifying tendency
+    int64_t cert_part_n_ = 0;      // capacity (workgroups)
 };
 
 }  // namespace qg

@@ -114,12 +114,21 @@ __device__ __forceinline__ TendBlock tend_block() {
 // j is computed (software pipeline), so HBM latency hides behind the stencil arithmetic.
 // Per interior point: read zeta, psi, [F(t-1), F(t-2)], write zeta+, F (+ ghost images).
 // ------------------------------------------------------------------------------------
-template <int TX, int PF, class T>
-__global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
+//
+// CERT (F64 PCG, one rank): the workgroup holds BOTH layers (threads [0, TX) layer 0, [TX, 2TX)
+// layer 1, each with its own rings) and also certifies the solve that produced psi from zeta:
+// per point and system, b_s = -(proj_in zeta)_s and r_s = b_s + (A_s psi~)_s with psi~ =
+// P_fwd^-1 psi, A_s psi~ = sum_l P_fwd^-1[s][l] (lap(psi_l) + alpha_s psi_l) (lap(psi_l) is
+// the ring's own), summed over the two layers through LDS; (b,b), (r,r) per workgroup.
+template <int TX, int PF, class T, bool CERT = false>
+__global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
     constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
+    constexpr int NL = CERT ? 2 : 1;       // layers per workgroup
     const TendBlock tb = tend_block();
-    const int layer = tb.z;
-    const int t = threadIdx.x;
+    // (wave-uniform: TX is a whole number of waves; in an SGPR the per-layer pointers stay
+    // scalar loads -- a per-lane index made them vector loads, re-issued every row)
+    const int layer = CERT ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x / TX)) : tb.z;
+    const int t = CERT ? (int)(threadIdx.x % TX) : (int)threadIdx.x;
     const int M = (int)a.M, P = (int)a.P;
     const int64_t ld = a.ld;
     const int x0 = tb.x * TX;
@@ -131,11 +140,42 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, i
     const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
     const int jb0 = r0 + (int)(((int64_t)yy * nr) / ny);
     const int jb1 = r0 + (int)(((int64_t)(yy + 1) * nr) / ny);
-    if (jb0 >= jb1) return;  // uniform over the block
+    if (jb0 >= jb1) {  // uniform over the block
+        if constexpr (CERT) {
+            if (threadIdx.x < 4) a.cert[4 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = 0;
+        }
+        return;
+    }
 
-    __shared__ T sp[RP][TX + 4];
-    __shared__ T sz[RZ][TX + 2];
-    __shared__ T sl[RL][TX + 2];
+    __shared__ T sp_[NL][RP][TX + 4];
+    __shared__ T sz_[NL][RZ][TX + 2];
+    __shared__ T sl_[NL][RL][TX + 2];
+    T(&sp)[RP][TX + 4] = sp_[CERT ? layer : 0];
+    T(&sz)[RZ][TX + 2] = sz_[CERT ? layer : 0];
+    T(&sl)[RL][TX + 2] = sl_[CERT ? layer : 0];
+    // CERT: layer 1's (b0, r0, b1, r1) contributions of row j, read by layer 0 after the next
+    // barrier (double-buffered by row parity); layer 0 keeps its own for that row meanwhile
+    __shared__ double xch[CERT ? 2 : 1][4][CERT ? TX : 1];
+    double cv[4] = {0, 0, 0, 0};  // (b0,b0), (r0,r0), (b1,b1), (r1,r1)
+    double pend[4] = {0, 0, 0, 0};
+    int pend_j = -1;
+    auto cert_fold = [&]() {  // layer 0: both layers' contributions of row pend_j
+        if (pend_j < 0) return;
+        const double *x = &xch[pend_j & 1][0][0];
+        double bs[2], rs[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bs[s] = pend[2 * s] + x[(2 * s) * TX + t];
+            rs[s] = pend[2 * s + 1] + x[(2 * s + 1) * TX + t];
+        }
+        if (a.cert_pin && i == 0 && pend_j == 0) bs[0] = rs[0] = 0.0;  // identity row: b = x = 0
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            cv[2 * s] += bs[s] * bs[s];
+            cv[2 * s + 1] += rs[s] * rs[s];
+        }
+        pend_j = -1;
+    };
 
     const T *psi = a.psi[layer];
     const T *zeta = a.zeta[layer];
@@ -264,6 +304,9 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, i
             if (jn < jb1) fetch_f(jn, f1[PF - 1], f2[PF - 1]);
         }
         __syncthreads();
+        if constexpr (CERT) {
+            if (layer == 0) cert_fold();  // row j-1: layer 1 wrote its part before this barrier
+        }
         if (more) lap_row(j + 2);
         if (has_out) {
             const T *Lm = sl[(j - 1 + 2 * RL) % RL], *L0 = sl[(j + 2 * RL) % RL], *Lp = sl[(j + 1 + 2 * RL) % RL];
@@ -295,6 +338,45 @@ __global__ __launch_bounds__(TX) void tendency_kernel(TendArgsT<T> a, int nyA, i
             const bool gr = a.write_ghost_rows;
             store_row_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
             store_row_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
+#ifndef QG_CERT_NOWORK  // (timing experiment: the two-layer structure without the check)
+            if constexpr (CERT) {  // this layer's parts of b_s and r_s at (i, j)
+                double part[4];
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const double b = -(a.cert_in[2 * s + layer] * (double)zcen);
+                    part[2 * s] = b;
+                    part[2 * s + 1] = b + a.cert_pinv[2 * s + layer] * ((double)L0[cl] + a.cert_alpha[s] * (double)P0[cp]);
+                }
+                if (layer == 1) {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) xch[j & 1][k][t] = part[k];
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) pend[k] = part[k];
+                    pend_j = j;
+                }
+            }
+#endif
+        }
+    }
+    if constexpr (CERT) {
+        __syncthreads();
+        if (layer == 0) cert_fold();
+        // workgroup sums (layer-1 waves add zeros), fixed order
+        __shared__ double sv[4][2 * TX / 64];
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            double v = cv[k];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+            if (lane == 0) sv[k][w] = v;
+        }
+        __syncthreads();
+        if (threadIdx.x < 4) {
+            double v = 0;
+            for (int g = 0; g < 2 * TX / 64; ++g) v += sv[threadIdx.x][g];
+            a.cert[4 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = v;
         }
     }
 }
@@ -733,6 +815,41 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     dim3 grid((unsigned)nx, (unsigned)(nyA + nyB), 2);
     tendency_kernel<TX, PF, T><<<grid, TX, 0, s>>>(a, nyA, nyB);
     QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+// The certifying variant (PCG, one rank): both layers per workgroup, chip-fulls as above.
+int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
+    constexpr int TX = 256, PF = 1;
+    static int sl = 0;
+    if (sl == 0) {
+        int dev = 0, cus = 0, per = 0;
+        QG_HIP(hipGetDevice(&dev));
+        QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_kernel<TX, PF, double, true>, 2 * TX, 0));
+        sl = cus * (per > 0 ? per : 1);
+    }
+    const int nx = (int)((a.M + TX - 1) / TX);
+    const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
+    const double pts = (double)a.M * (rA + rB);
+    static int ew = -1;
+    if (ew < 0) {
+        const char *e = std::getenv("QG_CERT_WAVES");
+        ew = e ? std::max(1, std::atoi(e)) : 0;
+        if (std::getenv("QG_CERT_VERBOSE")) std::fprintf(stderr, "cert tendency: %d resident per device\n", sl);
+    }
+    const int waves = ew ? ew : (pts >= 40.0e6 ? 4 : (pts >= 12.0e6 ? 3 : (pts >= 3.0e6 ? 1 : 2)));
+    const int target = std::max(1, waves * sl / nx);
+    auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
+    const int nyA = split(rA), nyB = split(rB);
+    if (nyA + nyB == 0) {
+        *nblk = 0;
+        return QG_OK;
+    }
+    dim3 grid((unsigned)nx, (unsigned)(nyA + nyB), 1);
+    tendency_kernel<TX, PF, double, true><<<grid, 2 * TX, 0, s>>>(a, nyA, nyB);
+    QG_LAUNCH_CHECK();
+    *nblk = (int)(grid.x * grid.y);
     return QG_OK;
 }
 

@@ -87,6 +87,9 @@ SIGNATURES = [
     ("qg_comm_init_host", C.c_int, [_vp, C.c_int, C.c_int, AllgatherFn, SendrecvFn, _vp]),
     ("qg_comm_set_timeout", C.c_int, [_vp, C.c_double]),
     ("qg_set_overlap", C.c_int, [_vp, C.c_int]),
+    ("qg_set_pcg_sync", C.c_int, [_vp, C.c_int]),
+    ("qg_pcg_certificate", C.c_int, [_vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                     C.POINTER(C.c_double)]),
     ("qg_comm_exchange_plan", C.c_int, [C.c_int, C.c_int, C.c_int * 2, C.c_int * 2, C.c_int * 2, C.c_int * 2]),
     ("qg_solver_create", C.c_int, [_i64, _i64, C.c_double, C.c_double * 2, C.c_int * 2,
                                    C.c_double * 4, C.c_double * 4, C.c_int, C.c_int, C.c_int, _vp,

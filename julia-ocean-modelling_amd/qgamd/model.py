@@ -248,6 +248,17 @@ class State:
         interior rows' tendency meanwhile (multi-rank only; bit-identical results)."""
         call("qg_set_overlap", self._ctx, 1 if on else 0)
 
+    def set_pcg_sync(self, sync=True):
+        """qg_set_pcg_sync: 1 = the host checks every PCG residual (and iterates when the
+        certificate fails); 0 = deferred on-device certification (default)."""
+        call("qg_set_pcg_sync", self._ctx, 1 if sync else 0)
+
+    def pcg_certificate(self):
+        """qg_pcg_certificate: deferred PCG certificates so far."""
+        n, f, first, worst = C.c_int64(), C.c_int64(), C.c_int64(), C.c_double()
+        call("qg_pcg_certificate", self._ctx, C.byref(n), C.byref(f), C.byref(first), C.byref(worst))
+        return {"solves": n.value, "failures": f.value, "first_failure": first.value, "worst_relres": worst.value}
+
     def _need_transport(self):
         if self.nranks != self._attached_ranks:
             raise RuntimeError(f"this state is slab {self.rank} of {self.nranks}: attach the {self.nranks}-rank "

@@ -77,6 +77,7 @@ def test_certification_failure_restarts_from_z0(env):
     restarts from x0 = z0 and stops at its stagnation floor; the answer is unchanged."""
     torch, qg, R, O = env
     st = qg.initialise_model(qg.bench_model(64, P=48), solver=1, pcg_rtol=1e-30, pcg_maxit=50)
+    st.set_pcg_sync(True)  # the host-checked form (the deferred default latches instead)
     for t in range(1, 5):
         st.step(t)
         s = st.stats()
@@ -95,3 +96,72 @@ def test_alpha_iteration_path(env, monkeypatch):
     assert s["iters"][0] == 1 and max(s["relres"]) < 1e-13
     ref = O.State(R.bench_model(64)).run(6)
     assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-10
+
+
+@pytest.mark.parametrize("N,steps", [(64, 9), (256, 7), (1024, 5)])
+def test_deferred_certificate_fused_in_tendency(env, N, steps):
+    """Default (deferred) certification: no host read per step; on one GPU each solve's
+    5-point residual is checked inside the next step's tendency (both layers per workgroup)
+    and latched on the device.  psi, zeta, f_store are bit-identical to the host-checked form,
+    every solve is certified (the last one by the stand-alone pass at the read), and the
+    latched residuals are at roundoff."""
+    torch, qg, R, O = env
+    m = qg.bench_model(N)
+    a = qg.run_model_no_output(m, nsteps=steps, solver=1)          # deferred (default)
+    b = qg.initialise_model(m, solver=1)
+    b.set_pcg_sync(True)
+    b.run(1, steps)
+    for n in ("psi", "zeta", "f_store"):
+        assert np.array_equal(a.to_numpy(n), b.to_numpy(n)), n
+    c = a.pcg_certificate()
+    assert c["solves"] == steps and c["failures"] == 0 and c["first_failure"] == 0, c
+    assert 0 < c["worst_relres"] < 1e-13, c
+    s = a.stats()
+    assert s["iters"] == [1, 1] and max(s["relres"]) < 1e-13, s
+    # the host-checked form's stand-alone pass: the same residual, at roundoff too
+    sb = b.stats()
+    assert sb["iters"] == [1, 1] and max(sb["relres"]) < 1e-13, sb
+
+
+def test_deferred_certificate_failure_is_reported(env):
+    """A target below the roundoff floor: every deferred certificate fails; the run is not
+    blocked, the next qg_synchronize reports QG_ERR_NOT_CONVERGED once, and the certificate
+    record counts the failures from the first solve on."""
+    torch, qg, R, O = env
+    st = qg.initialise_model(qg.bench_model(64), solver=1, pcg_rtol=1e-30)
+    st.run(1, 5)
+    with pytest.raises(qg.QGError) as e:
+        st.synchronize()
+    assert e.value.status == -7
+    st.synchronize()  # already reported
+    c = st.pcg_certificate()
+    assert c["solves"] == 5 and c["failures"] == 5 and c["first_failure"] == 1, c
+
+
+def test_deferred_pcg_graph_replay(env, monkeypatch):
+    """Deferred PCG steps have no host round trip, so qg_run replays them as HIP graphs:
+    bit-identical to launching them on the stream, all solves certified."""
+    torch, qg, R, O = env
+    m = qg.bench_model(128)
+    a = qg.run_model_no_output(m, nsteps=14, solver=1)
+    monkeypatch.setenv("QG_GRAPH", "1")
+    b = qg.run_model_no_output(m, nsteps=14, solver=1)
+    for n in ("psi", "zeta", "f_store"):
+        assert np.array_equal(a.to_numpy(n), b.to_numpy(n)), n
+    c = b.pcg_certificate()
+    assert c["solves"] == 14 and c["failures"] == 0, c
+
+
+def test_plain_cg_256(env):
+    """QG_PRECOND_NONE (plain CG) at 256^2, pcg_rtol 1e-12, pcg_maxit 3000: converges (or stops
+    at its roundoff floor <= 1e-10) and matches the oracle; the iteration count is reported."""
+    torch, qg, R, O = env
+    m = qg.bench_model(256)
+    st = qg.initialise_model(m, solver=1, precond=0, pcg_rtol=1e-12, pcg_maxit=3000)
+    for t in range(1, 3):
+        st.step(t)
+        s = st.stats()
+        print(f"plain CG 256^2 step {t}: iterations {s['iters']}, relres {s['relres']}")
+        assert 1 < s["iters"][0] < 3000 and max(s["relres"]) <= 1e-10, s
+    ref = O.State(R.bench_model(256)).run(2)
+    assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-8
