@@ -165,7 +165,16 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 #pragma unroll
             for (int p = 0; p < EP; ++p) in[p] = make_double2(p0 * c1[p] + p1 * c2[p], p2 * c1[p] + p3 * c2[p]);
             if (PF && j - DEPTH >= s0) load_into(j - DEPTH, c1, c2);
+#ifdef QG_EXP_NOFFT  // timing experiment only (wrong results): the row, untransformed
+            {
+                double2 *Zw = const_cast<double2 *>(Zb);
+#pragma unroll
+                for (int p = 0; p < EP; ++p) Zw[lay<Plan::LAST_NS>(t + p * T)] = in[p];
+                __syncthreads();
+            }
+#else
             FwdReg::run(in, b0, b1, twl);
+#endif
         } else {
 #pragma unroll
             for (int p = 0; p < EP; ++p) {
@@ -831,7 +840,14 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         }
         __syncthreads();
         double2 xo[Plan::R_LAST];  // last FFT pass output in registers: element t + r*T
+#ifdef QG_EXP_NOFFT
+        if constexpr (Plan::REG_OUT) {
+#pragma unroll
+            for (int p = 0; p < Plan::R_LAST; ++p) xo[p] = b0[t + p * T];
+        }
+#else
         Inv::run(b0, b1, twl, xo);
+#endif
         S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
         S *row1 = out1 + (size_t)(j + 1) * ld;
         const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;

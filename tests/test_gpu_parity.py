@@ -125,7 +125,8 @@ def test_reference_cubic_laplacian_on_device(torch, qg, R):
 
 def test_reference_arakawa_convergence_on_device(torch, qg, R):
     """test.jl:71-103 through qg_arakawa_J: errors dx*||J - J_true|| for M = 8 .. 256 equal the
-    known values and the slope is the notebook's -2.0171."""
+    survey-derived values (SURVEY 4's scratch run of the restatement: only the slope and the
+    ~0.85 first point are reference-held) and the slope is the notebook's -2.0171."""
     Lx = Ly = 10
     A = lambda x, y: np.sin(2 * np.pi * x / Lx) * np.sin(2 * np.pi * y / Ly)
     B = lambda x, y: np.cos(2 * np.pi * x / Lx) * np.cos(2 * np.pi * y / Ly)
