@@ -819,8 +819,10 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
 }
 
 // The certifying variant (PCG, one rank): both layers per workgroup, chip-fulls as above.
-int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
-    constexpr int TX = 256, PF = 1;
+// QG_CERT_TX = 128 / 256 (strip width), QG_CERT_WAVES = chip-fulls (tuning knobs).
+template <int TX>
+static int launch_tendency_cert_t(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
+    constexpr int PF = 1;
     static int sl = 0;
     if (sl == 0) {
         int dev = 0, cus = 0, per = 0;
@@ -828,6 +830,7 @@ int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
         QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_kernel<TX, PF, double, true>, 2 * TX, 0));
         sl = cus * (per > 0 ? per : 1);
+        if (std::getenv("QG_CERT_VERBOSE")) std::fprintf(stderr, "cert tendency TX %d: %d resident\n", TX, sl);
     }
     const int nx = (int)((a.M + TX - 1) / TX);
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
@@ -836,9 +839,10 @@ int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
     if (ew < 0) {
         const char *e = std::getenv("QG_CERT_WAVES");
         ew = e ? std::max(1, std::atoi(e)) : 0;
-        if (std::getenv("QG_CERT_VERBOSE")) std::fprintf(stderr, "cert tendency: %d resident per device\n", sl);
     }
-    const int waves = ew ? ew : (pts >= 40.0e6 ? 4 : (pts >= 12.0e6 ? 3 : (pts >= 3.0e6 ? 1 : 2)));
+    // two chip-fulls (tools/cert_sweep.sh, 4096^2: 1 to 6 chip-fulls within 4 %, 2 best)
+    (void)pts;
+    const int waves = ew ? ew : 2;
     const int target = std::max(1, waves * sl / nx);
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -851,6 +855,15 @@ int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
     QG_LAUNCH_CHECK();
     *nblk = (int)(grid.x * grid.y);
     return QG_OK;
+}
+
+int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
+    static int tx = -1;
+    if (tx < 0) {
+        const char *e = std::getenv("QG_CERT_TX");
+        tx = e ? std::atoi(e) : 128;  // (128 vs 256: 398 vs 401 us at 4096^2, same call)
+    }
+    return tx == 128 ? launch_tendency_cert_t<128>(a, nblk, s) : launch_tendency_cert_t<256>(a, nblk, s);
 }
 
 // Float32 default: the pair kernel over whole chip-fulls of 512-point strips (as above);
