@@ -47,9 +47,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=20,
                     help="untimed steps first (the GPU clock takes ~15 steps of 4096^2 to settle)")
-    ap.add_argument("--clock-warm-ms", type=float, default=300.0,
+    ap.add_argument("--clock-warm-ms", type=float, default=2000.0,
                     help="after the W warm-up steps, keep stepping (untimed) until this much wall "
-                         "time of GPU work has passed, so the timed region never sits in the clock ramp")
+                         "time of GPU work has passed, so the timed region never sits in the clock ramp "
+                         "(2 s: also long enough for a 1 Hz SMI sampler to see the GPU busy)")
     ap.add_argument("--n", "--grid", dest="n", type=int, default=4096, help="grid points per side per GPU")
     ap.add_argument("--dt", type=float, default=60.0)
     ap.add_argument("--chunk-rows", type=int, default=0)
@@ -110,7 +111,11 @@ def cpu_baseline(n, dt, steps, threads, steps_1t):
 
     el = timed(threads, steps)
     used = threads if threads > 0 else qg_oracle.lib().qgo_max_threads()
+    omp = os.environ.get("OMP_NUM_THREADS")
     out = {"value": steps / el, "unit": "timesteps/s", "cores": int(used), "kind": "port",
+           "threads_note": (f"OpenMP threads = OMP_NUM_THREADS={omp} (set by the GPU box: the host "
+                            f"CPU share of one GPU), of nproc={os.cpu_count()}" if omp and threads <= 0
+                            else "all threads OpenMP offers" if threads <= 0 else "--cpu-threads"),
            "sample": f"{steps} AB3 timesteps of the {n}x{n} F64 model (after its 2 Euler steps), "
                      f"C oracle (exact DFT solve), {el:.2f} s wall",
            "cpu": _cpu_model(), "nproc": os.cpu_count()}
@@ -211,7 +216,7 @@ def main():
     # clock up before the measured model's warm-up (single GPU only)
     pcg = None
     if args.pcg_steps > 0 and world == 1 and args.solver == "spectral" and args.dtype == "f64":
-        pcg = pcg_variant(qgamd, m, n, args.warmup, args.pcg_steps, torch, args.clock_warm_ms)
+        pcg = pcg_variant(qgamd, m, n, args.warmup, args.pcg_steps, torch, min(args.clock_warm_ms, 500.0))
 
     # W untimed warm-up steps (at least the 2 Euler steps + 1, so every timed step is an AB3
     # step that reads F(t-1), F(t-2)), then untimed steps until >= --clock-warm-ms of GPU work
@@ -300,13 +305,14 @@ def main():
     ms = el * 1e3 / K
     tend_gbs = BYTES_TENDENCY_AB3 * pts / (tend_ms * 1e-3) / 1e9
     step_gbs = BYTES_STEP * pts / (ms * 1e-3) / 1e9
-    traffic = None
+    traffic, pmc_tag = None, None
     prof = os.path.join(ROOT, "profiles", "pmc_tendency.json")
     if os.path.exists(prof):
         try:
             pj = json.load(open(prof))
             if pj.get("n") == n and args.dtype == "f64" and args.solver == "spectral":
                 traffic = pj.get("hbm_bytes_per_launch")
+                pmc_tag = pj.get("tag")
         except Exception:
             traffic = None
     out = {
@@ -348,6 +354,8 @@ def main():
             "unit": "GB/s",
             "frac": tend_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": ("profiles/pmc_tendency.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                               f"box {pmc_tag}" if traffic is not None else None),
             "avg_launch_ms": tend_ms,
             "algorithmic_bytes_per_launch": BYTES_TENDENCY_AB3 * pts,
         },
