@@ -36,8 +36,9 @@
  * Multi-GPU: the y-direction (second index) is split into slabs, one rank per GPU; every
  * rank passes its LOCAL P and binds local (M+2, P_local+2, 2, 3) arrays.  Halo rows move
  * with RCCL send/recv; the streamfunction inversion needs one small all-gather per step.
- * The ghost ROWS (memory rows 0 and P+1) of the fields a step writes are refreshed lazily:
- * grouped with the next step's halo exchange, or by qg_synchronize() / qg_canonicalize(),
+ * The ghost ROWS (memory rows 0 and P+1) of the fields a step writes are refreshed lazily
+ * (no kernel reads them; a step's exchange carries only the tendency's halo rows): by
+ * qg_synchronize() / qg_canonicalize() / qg_snapshot() / qg_diagnostics(), all slots at once,
  * which a caller invokes before reading the arrays (single GPU: always current).
  */
 #ifndef QG_MI355_H

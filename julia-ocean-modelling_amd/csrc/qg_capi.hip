@@ -18,6 +18,8 @@ int comm_destroy(void *comm);
 int comm_allgather(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
 int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
               hipStream_t s);
+int comm_halo_rows(void *comm, double *const *f2, int n2, int64_t ld, int64_t P, hipStream_t s,
+                   const double **rows_out);
 int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t ld,
                   int64_t P, hipStream_t s, bool ghost_f2);
 int comm_init(void **comm, int nranks, int rank, const char id[128]);
@@ -298,14 +300,15 @@ static void fill_wrap_rows(const qg_ctx *c, const T *base, RowSrcT<T> &rs) {
 }  // extern "C++"
 
 // ---- multi-GPU ghost rows --------------------------------------------------------------
-// the newest zeta, psi and F (both layers): the fields whose ghost rows a step leaves stale
-static int newest_fields(qg_ctx *c, double *f[6]) {
-    for (int l = 0; l < 2; ++l) {
-        f[l] = c->field(c->zeta, l, c->heads[0]);
-        f[2 + l] = c->field(c->psi, l, c->heads[1]);
-        f[4 + l] = c->field(c->fst, l, c->heads[2]);
-    }
-    return 6;
+// A step's exchange carries only the tendency's halo rows; the ghost rows (memory rows 0 and
+// P+1, the drop-in ghost ring) of every field a step writes are left stale -- no kernel reads
+// them -- and refreshed, all slots at once, when a caller needs the arrays (flush_ghosts).
+static int all_fields(qg_ctx *c, double *f[18]) {
+    int n = 0;
+    for (void *base : {c->zeta, c->psi, c->fst})
+        for (int slot = 0; slot < 3; ++slot)
+            for (int l = 0; l < 2; ++l) f[n++] = c->field(base, l, slot);
+    return n;
 }
 
 // every host wait of a context: bounded (watchdog) once a transport is attached
@@ -315,8 +318,8 @@ static int ctx_wait(qg_ctx *c, const char *what) {
 
 static int flush_ghosts(qg_ctx *c) {
     if (!c->distributed || !c->ghosts_pending) return QG_OK;
-    double *f[6];
-    const int n = newest_fields(c, f);
+    double *f[18];
+    const int n = all_fields(c, f);
     QG_CHECK(comm_exchange(c->comm, nullptr, 0, nullptr, f, n, c->row_words(), c->p.P, c->stream, false));
     c->ghosts_pending = false;
     return QG_OK;
@@ -372,20 +375,18 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
         }
         if (!done) QG_CHECK(launch_tendency(a, c->stream));
     } else {
-        // halo rows of psi (depth 2; zeta uses the inner two) from the neighbouring slabs,
-        // grouped with the pending ghost-row refresh of the previous step's outputs
+        // halo rows of psi (depth 2; zeta uses the inner two) from the neighbouring slabs, read
+        // by the tendency where they are received (comm_halo_rows: no unpack, no ghost rows)
         double *f2[4] = {c->field(c->psi, 0, ph), c->field(c->psi, 1, ph), c->field(c->zeta, 0, zh),
                          c->field(c->zeta, 1, zh)};
-        // (the f2 fields are the newest psi and zeta: their ghost rows come from the halo rows)
-        double *f1[2] = {c->field(c->fst, 0, fh), c->field(c->fst, 1, fh)};
-        const int n1 = c->ghosts_pending ? 2 : 0;
-        const int64_t row = p.M + 2;  // halo buffer: [field][4 rows][M+2 elements]; +1 = interior start
-        const T *hb = reinterpret_cast<const T *>(c->halo);
-        for (int l = 0; l < 2; ++l)
-            for (int h = 0; h < 4; ++h) {
-                a.psi_rows[l].halo[h] = hb + ((size_t)(l * 4 + h)) * row + 1;
-                a.zeta_rows[l].halo[h] = hb + ((size_t)((2 + l) * 4 + h)) * row + 1;
-            }
+        const double *hr[16];
+        auto set_halo = [&]() {  // (+1: the interior start of a received row)
+            for (int l = 0; l < 2; ++l)
+                for (int h = 0; h < 4; ++h) {
+                    a.psi_rows[l].halo[h] = reinterpret_cast<const T *>(hr[4 * l + h]) + 1;
+                    a.zeta_rows[l].halo[h] = reinterpret_cast<const T *>(hr[4 * (2 + l) + h]) + 1;
+                }
+        };
         if (c->overlap && p.P >= 8) {
             // exchange on the side stream, ordered after everything already queued on the
             // context's stream (the previous step's pass B, a ghost flush using the staging
@@ -398,10 +399,9 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
             }
             QG_HIP(hipEventRecord(c->ov_ready, c->stream));
             QG_HIP(hipStreamWaitEvent(c->ov_stream, c->ov_ready, 0));
-            QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, c->row_words(), p.P, c->ov_stream,
-                                   c->ghosts_pending));
+            QG_CHECK(comm_halo_rows(c->comm, f2, 4, c->row_words(), p.P, c->ov_stream, hr));
             QG_HIP(hipEventRecord(c->ov_halo, c->ov_stream));
-            c->ghosts_pending = false;
+            set_halo();
             TendArgsT<T> in = a;
             in.j0 = 2;
             in.j1 = (int)p.P - 2;
@@ -415,9 +415,8 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
             bd.j3 = (int)p.P;
             QG_CHECK(launch_tendency(bd, c->stream));
         } else {
-            QG_CHECK(comm_exchange(c->comm, f2, 4, c->halo, f1, n1, c->row_words(), p.P, c->stream,
-                                   c->ghosts_pending));
-            c->ghosts_pending = false;
+            QG_CHECK(comm_halo_rows(c->comm, f2, 4, c->row_words(), p.P, c->stream, hr));
+            set_halo();
             QG_CHECK(launch_tendency(a, c->stream));
         }
         c->ghosts_pending = true;
@@ -454,7 +453,7 @@ int qg_evolve_psi(qg_ctx *c) {
                                 c->distributed ? comm_allgather : nullptr, c->comm));
     }
     c->heads[1] = pn;
-    if (c->distributed) c->ghosts_pending = true;  // psi's ghost rows: with the next exchange
+    if (c->distributed) c->ghosts_pending = true;  // psi's ghost rows: at the next ghost flush
     return c->pcg ? c->last_status : QG_OK;
 }
 

@@ -219,6 +219,48 @@ int comm_set_timeout(void *comm, double seconds) {
     return QG_OK;
 }
 
+// The staging buffer [to_next | to_prev | from_prev | from_next], `rows` rows of ld words
+// each.  Allocated once for the largest exchange (XMAX / 2 rows per direction), so a later,
+// larger exchange never frees a buffer an earlier one's pending kernels still read.
+static int ensure_stage(Comm *c, int rows, int64_t ld, double *xbuf[4]) {
+    const size_t need = (size_t)4 * (XMAX / 2) * ld;
+    if (rows > XMAX / 2) return QG_ERR_INVALID_ARG;
+    if (need > c->stage_n) {
+        if (c->stage) {
+            QG_HIP(hipDeviceSynchronize());  // (a wider row length: a new context shape)
+            (void)hipFree(c->stage);
+        }
+        c->stage = nullptr;
+        c->stage_n = 0;
+        QG_HIP(hipMalloc((void **)&c->stage, sizeof(double) * need));
+        c->stage_n = need;
+    }
+    for (int b = 0; b < 4; ++b) xbuf[b] = c->stage + (size_t)b * rows * ld;
+    return QG_OK;
+}
+
+// the grouped send / receive of one exchange (the plan of exchange_plan), cnt words each
+static int post(Comm *c, double *const xbuf[4], int64_t cnt, hipStream_t s) {
+    int speer[2], sbuf[2], rpeer[2], rbuf[2];
+    exchange_plan(c->rank, c->nranks, speer, sbuf, rpeer, rbuf);
+    if (c->sr) {
+        const double *sp[2] = {xbuf[sbuf[0]], xbuf[sbuf[1]]};
+        double *rp[2] = {xbuf[rbuf[0]], xbuf[rbuf[1]]};
+        const int64_t sc[2] = {cnt, cnt}, rcnt[2] = {cnt, cnt};
+        if (c->sr(c->user, 2, sp, sc, speer, 2, rp, rcnt, rpeer, s) != 0) {
+            std::fprintf(stderr, "qg_mi355 rank %d/%d: host transport sendrecv failed\n", c->rank, c->nranks);
+            c->failed = true;
+            return QG_ERR_RCCL;
+        }
+        return QG_OK;
+    }
+    QG_NCCL(ncclGroupStart());
+    for (int k = 0; k < 2; ++k) QG_NCCL(ncclSend(xbuf[sbuf[k]], (size_t)cnt, ncclDouble, speer[k], c->nccl, s));
+    for (int k = 0; k < 2; ++k) QG_NCCL(ncclRecv(xbuf[rbuf[k]], (size_t)cnt, ncclDouble, rpeer[k], c->nccl, s));
+    QG_NCCL(ncclGroupEnd());
+    return QG_OK;
+}
+
 // One exchange with the two ring neighbours, as ONE message per direction: the rows are
 // packed into a staging buffer per neighbour, sent / received in one group, and unpacked.
 //   f2[0..n2): depth-2 halo -> halo_buf[f][4][M+2] = rows -2,-1 (from rank-1), P,P+1 (from
@@ -235,18 +277,8 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
     const int rows = 2 * n2 + n1;  // rows per direction
     if (n2 < 0 || n1 < 0 || 4 * n2 + (ghost_f2 ? 2 * n2 : 0) + 2 * n1 > XMAX) return QG_ERR_INVALID_ARG;
     if (rows == 0) return QG_OK;
-    int speer[2], sbuf[2], rpeer[2], rbuf[2];
-    exchange_plan(c->rank, c->nranks, speer, sbuf, rpeer, rbuf);
-    const size_t need = (size_t)4 * rows * ld;
-    if (need > c->stage_n) {
-        if (c->stage) (void)hipFree(c->stage);
-        c->stage = nullptr;
-        c->stage_n = 0;
-        QG_HIP(hipMalloc((void **)&c->stage, sizeof(double) * need));
-        c->stage_n = need;
-    }
     double *xbuf[4];  // indexed by QG_XBUF_*
-    for (int b = 0; b < 4; ++b) xbuf[b] = c->stage + (size_t)b * rows * ld;
+    QG_CHECK(ensure_stage(c, rows, ld, xbuf));
     double *to_next = xbuf[QG_XBUF_TO_NEXT], *to_prev = xbuf[QG_XBUF_TO_PREV];
     double *from_prev = xbuf[QG_XBUF_FROM_PREV], *from_next = xbuf[QG_XBUF_FROM_NEXT];
     RowCopies pk{}, up{};
@@ -274,23 +306,39 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
         up.src[up.n] = from_next + r * ld;     up.dst[up.n++] = b + fidx(0, P + 1, ld);
     }
     QG_CHECK(copy_rows(pk, s));
-    const int64_t cnt = (int64_t)rows * ld;
-    if (c->sr) {
-        const double *sp[2] = {xbuf[sbuf[0]], xbuf[sbuf[1]]};
-        double *rp[2] = {xbuf[rbuf[0]], xbuf[rbuf[1]]};
-        const int64_t sc[2] = {cnt, cnt}, rcnt[2] = {cnt, cnt};
-        if (c->sr(c->user, 2, sp, sc, speer, 2, rp, rcnt, rpeer, s) != 0) {
-            std::fprintf(stderr, "qg_mi355 rank %d/%d: host transport sendrecv failed\n", c->rank, c->nranks);
-            c->failed = true;
-            return QG_ERR_RCCL;
-        }
-    } else {
-        QG_NCCL(ncclGroupStart());
-        for (int k = 0; k < 2; ++k) QG_NCCL(ncclSend(xbuf[sbuf[k]], (size_t)cnt, ncclDouble, speer[k], c->nccl, s));
-        for (int k = 0; k < 2; ++k) QG_NCCL(ncclRecv(xbuf[rbuf[k]], (size_t)cnt, ncclDouble, rpeer[k], c->nccl, s));
-        QG_NCCL(ncclGroupEnd());
-    }
+    QG_CHECK(post(c, xbuf, (int64_t)rows * ld, s));
     return copy_rows(up, s, c->progress_d, ++c->seq);
+}
+
+// The halo rows of the tendency only, left where they are received: no unpack kernel (the
+// tendency reads them from the staging buffer) and no ghost rows (refreshed by the next
+// ghost flush).  rows_out[4 f + h] = row h of field f (h: -2, -1, P, P+1).  The pack kernel
+// publishes the watchdog's progress: every earlier exchange has completed when it runs.
+int comm_halo_rows(void *comm, double *const *f2, int n2, int64_t ld, int64_t P, hipStream_t s,
+                   const double **rows_out) {
+    Comm *c = static_cast<Comm *>(comm);
+    if (!c || c->failed || (!c->nccl && !c->sr)) return QG_ERR_RCCL;
+    const int rows = 2 * n2;
+    if (n2 < 1 || 2 * rows > XMAX) return QG_ERR_INVALID_ARG;
+    double *xbuf[4];
+    QG_CHECK(ensure_stage(c, rows, ld, xbuf));
+    double *to_next = xbuf[QG_XBUF_TO_NEXT], *to_prev = xbuf[QG_XBUF_TO_PREV];
+    const double *from_prev = xbuf[QG_XBUF_FROM_PREV], *from_next = xbuf[QG_XBUF_FROM_NEXT];
+    RowCopies pk{};
+    pk.ld = ld;
+    for (int f = 0; f < n2; ++f) {
+        double *b = f2[f];
+        for (int q = 0; q < 2; ++q) {
+            const int r = 2 * f + q;
+            pk.src[pk.n] = b + fidx(0, P - 1 + q, ld); pk.dst[pk.n++] = to_next + r * ld;  // rows P-2, P-1
+            pk.src[pk.n] = b + fidx(0, 1 + q, ld);     pk.dst[pk.n++] = to_prev + r * ld;  // rows 0, 1
+            rows_out[4 * f + q] = from_prev + r * ld;                                      // rows -2, -1
+            rows_out[4 * f + 2 + q] = from_next + r * ld;                                  // rows P, P+1
+        }
+    }
+    QG_CHECK(copy_rows(pk, s, c->progress_d, c->seq));
+    ++c->seq;
+    return post(c, xbuf, (int64_t)rows * ld, s);
 }
 
 // depth == 2: halo rows into halo_buf; depth == -1: ghost-row refresh in place
