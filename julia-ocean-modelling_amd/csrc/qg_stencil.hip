@@ -245,7 +245,11 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
         }
     };
 
-    // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 straight into LDS
+    // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 into LDS.  All eight rows' loads
+    // are issued before the first LDS write (a fetch-commit loop waited one full memory latency
+    // per row: eight round trips in front of every strip, while the workgroups of a chip-full,
+    // which start together, all sat in them); QG_TEND_SERIAL_PROLOGUE restores that order.
+#ifdef QG_TEND_SERIAL_PROLOGUE
     for (int j = jb0 - 2; j <= jb0 + 2; ++j) {
         T c = 0, h = 0;
         fetch_psi(j, c, h);
@@ -256,6 +260,25 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
         fetch_zeta(j, c, h);
         commit_zeta(j, c, h);
     }
+#else
+    {
+        T p0c[5], p0h[5], z0c[3], z0h[3];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            p0c[k] = p0h[k] = 0;
+            fetch_psi(jb0 - 2 + k, p0c[k], p0h[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            z0c[k] = z0h[k] = 0;
+            fetch_zeta(jb0 - 1 + k, z0c[k], z0h[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) commit_psi(jb0 - 2 + k, p0c[k], p0h[k]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) commit_zeta(jb0 - 1 + k, z0c[k], z0h[k]);
+    }
+#endif
     // prefetch for iterations jb0 .. jb0+PF-1: psi row j+3, zeta row j+2 (committed while
     // rows are still needed, i.e. j+2 <= jb1) and F of row j
 #pragma unroll
@@ -527,7 +550,9 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
             dst[W + 2] = ((((p0[W + 1] + p0[W + 3]) - T(4) * p0[W + 2]) + pm[W + 2]) + pp[W + 2]) * idx2;
     };
 
-    // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 straight into LDS
+    // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 into LDS, every load issued
+    // before the first LDS write (see tendency_kernel)
+#ifdef QG_TEND_SERIAL_PROLOGUE
     for (int j = jb0 - 2; j <= jb0 + 2; ++j) {
         V c = {0, 0}, h = {0, 0};
         fetch_psi(j, c, h);
@@ -538,6 +563,25 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
         fetch_zeta(j, c, h);
         commit(sz[ring(j, RZ)], c, h);
     }
+#else
+    {
+        V p0c[5], p0h[5], z0c[3], z0h[3];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            p0c[k] = p0h[k] = V{0, 0};
+            fetch_psi(jb0 - 2 + k, p0c[k], p0h[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            z0c[k] = z0h[k] = V{0, 0};
+            fetch_zeta(jb0 - 1 + k, z0c[k], z0h[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) commit(sp[ring(jb0 - 2 + k, RP)], p0c[k], p0h[k]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) commit(sz[ring(jb0 - 1 + k, RZ)], z0c[k], z0h[k]);
+    }
+#endif
     if (jb0 + 2 <= jb1) {
         fetch_psi(jb0 + 3, pc, ph);
         fetch_zeta(jb0 + 2, zc, zh);
@@ -805,10 +849,11 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     // read before the first output row) then costs less than the idle tail of a second wave
     // (tile sweep, profiles/r01/tile_sweep_*.json: 2048^2 106 vs 111 us)
     const double pts = (double)a.M * (rA + rB);
-    // four chip-fulls at 8192^2 and up (tools/tend_waves.sh: 1 422 -> 1 349 us), three at
-    // 4096^2 (after the F-wait fix: 356.1 -> 352.0 us, three A/B pairs, tools/tend_waves_ab.sh)
-    const int waves = env_waves ? env_waves
-                                : (pts >= 40.0e6 ? 4 : (pts >= 12.0e6 ? 3 : (pts >= 3.0e6 ? 1 : 2)));
+    // six chip-fulls from ~3500^2 up: with the batched ring prologue a strip's start costs one
+    // memory latency, and shorter strips keep the chip's concurrent accesses closer together
+    // (tools/waves_sweep.sh, profiles/r02/prologue: 4096^2 3 -> 6 chip-fulls 341.7 -> 335 us,
+    // 8192^2 4 -> 6 1 237-1 257 -> 1 230-1 241 us; before the prologue fix three and four)
+    const int waves = env_waves ? env_waves : (pts >= 12.0e6 ? 6 : (pts >= 3.0e6 ? 1 : 2));
     const int target = std::max(1, waves * sl / (2 * nx));  // row workgroups per column strip
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -840,9 +885,10 @@ static int launch_tendency_cert_t(const TendArgsT<double> &a, int *nblk, hipStre
         const char *e = std::getenv("QG_CERT_WAVES");
         ew = e ? std::max(1, std::atoi(e)) : 0;
     }
-    // two chip-fulls (tools/cert_sweep.sh, 4096^2: 1 to 6 chip-fulls within 4 %, 2 best)
+    // three chip-fulls (tools/sweep_r02g.sh, 4096^2 with the batched prologue: 2 -> 3
+    // 388.8 -> 385.1 us, 2 to 8 within 2 %; before it 2 was best, tools/cert_sweep.sh)
     (void)pts;
-    const int waves = ew ? ew : 2;
+    const int waves = ew ? ew : 3;
     const int target = std::max(1, waves * sl / nx);
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -883,7 +929,9 @@ static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
     const int nx = (int)((a.M + W - 1) / W);
     // four chip-fulls at 8192^2 and up (tools/tend_waves_f32.sh: 797 -> 766 us)
     const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
-    const int waves = e ? std::max(1, std::atoi(e)) : (pts >= 40.0e6 ? 4 : 2);
+    // (tools/sweep_r02g.sh with the batched prologue: 8192^2 4 -> 6 chip-fulls 773 -> 764 us;
+    // 4096^2 keeps 2: 209 vs 213-230 us)
+    const int waves = e ? std::max(1, std::atoi(e)) : (pts >= 40.0e6 ? 6 : 2);
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
     const int target = std::max(1, waves * sl / (2 * nx));
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
