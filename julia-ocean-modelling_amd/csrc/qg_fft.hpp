@@ -155,6 +155,49 @@ __device__ __forceinline__ void fft_init_twiddles(double2 *twl, const double2 *_
     fill_twiddles<N, T, 1>(twl, tw, threadIdx.x);
 }
 
+// The same fill in two halves.  fft_init_twiddles issues one load per pass and writes it to
+// LDS before the next pass's load goes out: one memory latency per pass, in front of a
+// kernel's first row.  fft_twiddle_load issues all of this thread's loads (flat entry e of the
+// LDS tables -> global index tw_src(e)); the caller then issues its own first loads and calls
+// fft_twiddle_store before its first barrier, so the latencies overlap.
+template <int N, int T>
+struct TwFill {
+    static constexpr int TW = FftPlan<N, T>::TW;
+    static constexpr int PER = (TW + T - 1) / T > 0 ? (TW + T - 1) / T : 1;
+    double2 v[PER];
+};
+template <int N, int T, int NS>
+__device__ __forceinline__ int tw_src(int e) {  // e >= tw_off<NS>()
+    if constexpr (NS >= N) {
+        return 0;
+    } else {
+        using P = Passes<N, T, NS>;
+        constexpr int R = P::R, S = N / (NS * R), off = FftPlan<N, T>::template tw_off<NS>();
+        if (P::tw_here > 0 && e < off + P::tw_here) {
+            const int l = e - off;
+            if constexpr (NS <= 256) return l * S;
+            else return l < 64 ? l * S : 64 * (l - 64) * S;
+        }
+        return tw_src<N, T, NS * R>(e);
+    }
+}
+template <int N, int T>
+__device__ __forceinline__ void fft_twiddle_load(TwFill<N, T> &f, const double2 *__restrict__ tw) {
+#pragma unroll
+    for (int p = 0; p < TwFill<N, T>::PER; ++p) {
+        const int e = threadIdx.x + p * T;
+        if (e < TwFill<N, T>::TW) f.v[p] = tw[tw_src<N, T, 1>(e)];
+    }
+}
+template <int N, int T>
+__device__ __forceinline__ void fft_twiddle_store(double2 *twl, const TwFill<N, T> &f) {
+#pragma unroll
+    for (int p = 0; p < TwFill<N, T>::PER; ++p) {
+        const int e = threadIdx.x + p * T;
+        if (e < TwFill<N, T>::TW) twl[e] = f.v[p];
+    }
+}
+
 // One pass: butterflies j = t, t + T, ...; reads `src` (layout of the writer with stride
 // IN_NS) or registers `io` (FROM_REG), writes `dst` with layout lay<NS> then a barrier, or
 // leaves the result in `io` (TO_REG, no barrier).

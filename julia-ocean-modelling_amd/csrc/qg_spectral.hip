@@ -90,10 +90,21 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     double2 *b0 = lds, *b1 = Plan::PINGPONG ? lds + LdsSize<N>::value : lds,
             *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
     const double2 *Zb = RES_B1 ? b1 : b0;
+    // set-up loads first (twiddles, r of the real line k = N/2 (see spec_passB), the first
+    // row), their LDS writes after: one memory latency in front of the first row, not one per
+    // load (QG_PA_SERIAL_HEAD restores the serial head)
+#ifdef QG_PA_SERIAL_HEAD
     fft_init_twiddles<N, T>(twl, a.tw);
-    __shared__ double crN[2];  // r of the real line k = N/2 (see spec_passB)
+    __shared__ double crN[2];
     if (threadIdx.x < 2) crN[threadIdx.x] = QG_CR(threadIdx.x * a.KS + NH);
     __syncthreads();
+#else
+    TwFill<N, T> twf;
+    fft_twiddle_load<N, T>(twf, a.tw);
+    __shared__ double crN[2];
+    double crv = 0;
+    if (threadIdx.x < 2) crv = QG_CR(threadIdx.x * a.KS + NH);
+#endif
     const int t = threadIdx.x, c = blockIdx.x;
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
@@ -232,12 +243,22 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     if constexpr (DEPTH == 2) {
         load_into(e, pf1, pf2);
         if (e - 1 >= s0) load_into(e - 1, qf1, qf2);
+#ifndef QG_PA_SERIAL_HEAD
+        fft_twiddle_store<N, T>(twl, twf);
+        if (threadIdx.x < 2) crN[threadIdx.x] = crv;
+        __syncthreads();
+#endif
         for (int j = e; j >= s0; j -= 2) {
             row_step(j, pf1, pf2);
             if (j - 1 >= s0) row_step(j - 1, qf1, qf2);
         }
     } else {
         if constexpr (PF) load_into(e, pf1, pf2);
+#ifndef QG_PA_SERIAL_HEAD
+        fft_twiddle_store<N, T>(twl, twf);
+        if (threadIdx.x < 2) crN[threadIdx.x] = crv;
+        __syncthreads();
+#endif
         for (int j = e; j >= s0; --j) row_step(j, pf1, pf2);
     }
 #pragma unroll
@@ -415,6 +436,22 @@ __device__ double pin_line(const SpecArgs &a, int s, int k, double delta) {
         pin_part = (2 * k == a.M) ? X : 2 * X;
     }
     return pin_part;
+}
+
+// carry-in state of line (s, k) entering chunk c: cu = r^L u_in, w = w_in (see header), from
+// the chunk's zero-closure carries (UIN_c, WIN_c) and the line's closure (Ue, We)
+__device__ __forceinline__ void carry_in(const SpecArgs &a, const Coef &cf, int s, int c, double delta, bool inject,
+                                         double2 Ue, double2 We, double2 uinc, double2 winc, double2 &cu,
+                                         double2 &w) {
+    const int64_t n = (int64_t)c * a.L;
+    const double2 uin = cfma(exp((double)(a.Nc - 1 - c) * a.L * cf.lr), Ue, uinc);
+    cu = cscale(uin, cf.q);
+    double gc = 0;
+    if (n > 0) gc = exp((double)(a.P - n + 1) * cf.lr) * (expm1(2.0 * n * cf.lr) / expm1(2.0 * cf.lr));
+    double2 wi = cfma(gc, Ue, winc);
+    wi = cfma(exp((double)n * cf.lr), We, wi);
+    if (s == 0 && inject && c >= 1) wi.x += exp((double)(n - 1) * cf.lr) * (cf.cs * delta);
+    w = wi;
 }
 
 // ------------------------------------------------------------------------------------
@@ -669,25 +706,16 @@ __device__ __forceinline__ double pin_total(double p, double *pinw) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-// carry-in state of line (s, k) entering chunk c: cu = r^L u_in, w = w_in (see header)
 __device__ __forceinline__ void chunk_carry(const SpecArgs &a, int s, int k, int c, double delta, bool inject,
                                             double2 &cu, double2 &w) {
 #ifdef QG_EXP_NOPROLOGUE  // timing experiment only (wrong results)
     cu = w = make_double2(0, 0);
     return;
 #endif
-
+    const size_t o = ((size_t)c * 2 + s) * a.KS + k;
     const Coef cf = a.coef[s * a.KS + k];
     const double2 Ue = a.EXT[(size_t)s * a.KS + k], We = a.EXT[(size_t)(2 + s) * a.KS + k];
-    const int64_t n = (int64_t)c * a.L;
-    const double2 uin = cfma(exp((double)(a.Nc - 1 - c) * a.L * cf.lr), Ue, a.UIN[((size_t)c * 2 + s) * a.KS + k]);
-    cu = cscale(uin, cf.q);
-    double gc = 0;
-    if (n > 0) gc = exp((double)(a.P - n + 1) * cf.lr) * (expm1(2.0 * n * cf.lr) / expm1(2.0 * cf.lr));
-    double2 wi = cfma(gc, Ue, a.WIN[((size_t)c * 2 + s) * a.KS + k]);
-    wi = cfma(exp((double)n * cf.lr), We, wi);
-    if (s == 0 && inject && c >= 1) wi.x += exp((double)(n - 1) * cf.lr) * (cf.cs * delta);
-    w = wi;
+    carry_in(a, cf, s, c, delta, inject, Ue, We, a.UIN[o], a.WIN[o], cu, w);
 }
 
 template <int N, class S>
@@ -701,7 +729,15 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     double2 *b0 = lds, *b1 = Plan::PINGPONG ? lds + LdsSize<N>::value : lds,
             *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
     const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
+    // set-up loads (twiddles, the chunk's singular-line values, (r, 1/r) of k = N/2) go out
+    // first and reach LDS just before pin_total's barrier (QG_PB_SERIAL_HEAD: the serial head,
+    // one memory latency per load in front of the first row's loads)
+#ifdef QG_PB_SERIAL_HEAD
     fft_init_twiddles<N, T>(twl, a.tw);
+#else
+    TwFill<N, T> twf;
+    fft_twiddle_load<N, T>(twf, a.tw);
+#endif
     const int t = threadIdx.x, c = blockIdx.x;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     // the chunk's values of the singular line, staged once (a global load per row would sit
@@ -712,8 +748,15 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     // that owns slot (0, 0), whose global load there would wait (in-order vmcnt) for the
     // next row's prefetch, and the whole workgroup for that wave at the next barrier
     __shared__ double2 crN[2];
+#ifdef QG_PB_SERIAL_HEAD
     if (a.pinned0 && t < L) lline[t] = a.line[s0 + t];
     if (N < 4096 && t < 2) crN[t] = QG_CRR(t * a.KS + NH);
+#else
+    double llv = 0;
+    double2 crv = make_double2(0, 0);
+    if (a.pinned0 && t < L) llv = a.line[s0 + t];
+    if (N < 4096 && t < 2) crv = QG_CRR(t * a.KS + NH);
+#endif
     const double pinp = a.pinned0 ? pin_part<T>(a, t) : 0.0;  // (lline, twl: see pin_total)
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
@@ -783,6 +826,11 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     // folded after the chunk set-up, so the carries' loads are not queued behind the pin
     // parts' (folding first: 4096^2 pass B 125.9 -> 137.9 us); its barrier also publishes
     // lline and the twiddles
+#ifndef QG_PB_SERIAL_HEAD
+    fft_twiddle_store<N, T>(twl, twf);
+    if (a.pinned0 && t < L) lline[t] = llv;
+    if (N < 4096 && t < 2) crN[t] = crv;
+#endif
     const double pin = pin_total<T>(pinp, pinw);
     if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     for (int j = s0; j <= e; ++j) {
