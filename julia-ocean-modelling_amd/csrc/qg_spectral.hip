@@ -960,11 +960,19 @@ __device__ __forceinline__ double2 half_tw(const double2 *wlo, const double2 *wh
 }
 
 __device__ __forceinline__ void half_lds_init(const SpecArgs &a, double2 *twl, double2 *wlo, double2 *whi) {
-    fft_init_twiddles<HN, HT>(twl, a.tw2);
+    // every load in flight before the first LDS write (one memory latency, not one per table)
+    TwFill<HN, HT> twf;
+    fft_twiddle_load<HN, HT>(twf, a.tw2);
     const int t = threadIdx.x;
+    double2 lo = make_double2(0, 0), hi = make_double2(0, 0);
     if (t < 64) {
-        wlo[t] = a.tw[t];
-        whi[t] = a.tw[64 * t];
+        lo = a.tw[t];
+        hi = a.tw[64 * t];
+    }
+    fft_twiddle_store<HN, HT>(twl, twf);
+    if (t < 64) {
+        wlo[t] = lo;
+        whi[t] = hi;
     }
 }
 
