@@ -150,11 +150,29 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     constexpr int DEPTH = 1;
 #endif
     double qf1[EP], qf2[EP];
+#if !defined(QG_PA_COEF_ROW) && !defined(QG_PA_COEF_LATE) && !defined(QG_PA_PF2)
+    // r of this thread's lines, loaded once: row-invariant, and at this kernel's register
+    // budget (224 VGPRs before) the eight values fit without spilling, so no row reloads them
+    // from L2 (QG_PA_COEF_ROW: reload per row, the old form)
+    constexpr bool COEF_HOIST = N >= 2048 && N <= 4096;
+#else
+    constexpr bool COEF_HOIST = false;
+#endif
+    double rqh[KQ][2];
+    if constexpr (COEF_HOIST) {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int k = t + q * T;
+                rqh[q][s] = (NH % T == 0 || k < NH) ? QG_CR(s * KS + k) : 0.0;
+            }
+    }
     // one row: consume the prefetched row (c1, c2), refill them with row j - DEPTH, transform,
     // split, filter
     auto row_step = [&](int j, auto &c1, auto &c2) {
         if constexpr (!PF) load_into(j, c1, c2);
-        asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
+        if constexpr (!COEF_HOIST) asm volatile("" ::: "memory");  // keep coefficient loads in the loop (see pass B)
         // this row's r, issued ahead of the next row's prefetch: loads complete in order
         // (vmcnt), so r loaded after the prefetch would make the recurrence wait for the
         // whole next row
@@ -165,7 +183,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
                 const int k = t + q * T;
-                if (NH % T == 0 || k < NH) rq[q][s] = QG_CR(s * KS + k);
+                if constexpr (COEF_HOIST) rq[q][s] = rqh[q][s];
+                else if (NH % T == 0 || k < NH) rq[q][s] = QG_CR(s * KS + k);
             }
 #define QG_PA_R(q, s, o) rq[q][s]
 #else
