@@ -152,9 +152,9 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     double qf1[EP], qf2[EP];
 #if !defined(QG_PA_COEF_ROW) && !defined(QG_PA_COEF_LATE) && !defined(QG_PA_PF2)
     // r of this thread's lines, loaded once: row-invariant, and at this kernel's register
-    // budget (224 VGPRs before) the eight values fit without spilling, so no row reloads them
-    // from L2 (QG_PA_COEF_ROW: reload per row, the old form)
-    constexpr bool COEF_HOIST = N >= 2048 && N <= 4096;
+    // budget (224 VGPRs before at 4096) the values fit without spilling, so no row reloads
+    // them from L2 (QG_PA_COEF_ROW: reload per row, the old form; below 1024 no gain measured)
+    constexpr bool COEF_HOIST = N >= 1024 && N <= 4096;
 #else
     constexpr bool COEF_HOIST = false;
 #endif
