@@ -77,6 +77,14 @@ def parse():
     ap.add_argument("--overlap", action="store_true",
                     help="N > 1 (or --comm-self): post the halo exchange on a second stream while the "
                          "interior rows' tendency runs (qg_set_overlap; bit-identical results)")
+    ap.add_argument("--dropin-steps", type=int, default=20,
+                    help="also time this many steps through the reference's own array signatures "
+                         "(evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(...) on bare arrays, "
+                         "slot 1 newest after every call; single GPU, F64 spectral; 0 = skip)")
+    ap.add_argument("--comm-probe-reps", type=int, default=20,
+                    help="N > 1 (or --comm-self): time the halo exchange and the record all-gather in "
+                         "isolation, this many calls each (0 = skip); also re-times the K steps with the "
+                         "halo overlap toggled (overlap_ab)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
@@ -156,6 +164,74 @@ def pcg_variant(qgamd, m, n, warmup, K, torch, warm_ms=300.0):
             "note": "same workload, evolve_psi! by PCG (spectral preconditioner, certified first step; "
                     "the 5-point residual check of every solve runs on the device, fused into the next "
                     "step's tendency, verdict latched there -- no host round trip)"}
+
+
+def dropin_variant(qgamd, m, n, warmup, K, torch):
+    """The drop-in path: the reference's loop body on bare (M+2, P+2, 2, 3) device arrays,
+    evolve_zeta!(model, zeta, psi, t, f_store) then evolve_psi!(model, zeta, psi, P, H)
+    (model.jl:155, :172), each call leaving slot 1 = newest as store_new_state! does (the
+    history shifted in place on the device).  K timed steps after the warm-up."""
+    src = qgamd.State(m, P_local=n)
+    src.initialise()
+    zeta, psi, f_store = src.zeta, src.psi, src.f_store  # (heads 0 after initialise)
+    pc = qgamd.get_poisson_cholesky(m.M, m.P, m.dx)
+    hc = qgamd.get_helmholtz_cholesky(m.M, m.P, m.dx, qgamd.S_eig(m))
+    t = 1
+    for _ in range(max(warmup, 3)):
+        qgamd.evolve_zeta_(m, zeta, psi, t, f_store)
+        qgamd.evolve_psi_(m, zeta, psi, pc, hc)
+        t += 1
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        qgamd.evolve_zeta_(m, zeta, psi, t, f_store)
+        qgamd.evolve_psi_(m, zeta, psi, pc, hc)
+        t += 1
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    qgamd.unbind(zeta, psi, f_store)
+    del src
+    return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K,
+            "note": "reference array signatures from Python (ctypes per call), slot order kept on every "
+                    "call by an in-place history shift (2 slot copies per field per step, as "
+                    "store_new_state! copies)"}
+
+
+# the JSON line's contract (the driver's fields + this bench's sub-records); checked before
+# printing and by tests/test_bench_schema_cpu.py against committed outputs
+_REQUIRED = {"metric": str, "value": float, "unit": str, "n_gpus": int, "steps": int, "warmup": int,
+             "ms_per_step": float, "higher_is_better": bool, "scaling": str, "dtype": str, "data": str,
+             "config": dict, "roofline": dict, "cpu_baseline": (dict, type(None))}
+_ROOFLINE = ("bound", "achieved", "peak", "unit", "frac", "traffic")
+_COMM = {"halo_ms": float, "halo_bytes_sent": int, "allgather_ms": float, "allgather_bytes_received": int,
+         "reps": int, "share_of_step": float}
+_OVERLAP_AB = {"halo_overlap": bool, "value": float, "ms_per_step": float, "steps": int}
+
+
+def validate_record(out):
+    """Raise ValueError if the bench record misses a field of its contract."""
+    def need(d, spec, where):
+        for k, t in spec.items():
+            if k not in d:
+                raise ValueError(f"{where}: missing {k}")
+            ok = isinstance(d[k], t) if not (t is float) else isinstance(d[k], (int, float))
+            if not ok or isinstance(d[k], bool) and t is not bool and t is not (dict, type(None)):
+                raise ValueError(f"{where}: {k} has type {type(d[k]).__name__}")
+    need(out, _REQUIRED, "record")
+    if out["metric"] != METRIC:
+        raise ValueError("record: metric differs from BASELINE.json's")
+    if "workload" not in out["config"]:
+        raise ValueError("config: missing workload")
+    for k in _ROOFLINE:
+        if k not in out["roofline"]:
+            raise ValueError(f"roofline: missing {k}")
+    multi = out["n_gpus"] > 1 or "1-rank" in str(out["config"].get("parallelism", ""))
+    if multi and out["config"].get("solver", "").startswith("spectral"):
+        for key, spec in (("comm", _COMM), ("overlap_ab", _OVERLAP_AB)):
+            if key not in out:
+                raise ValueError(f"multi-GPU record: missing {key}")
+            need(out[key], spec, key)
+    return True
 
 
 def main():
@@ -295,6 +371,41 @@ def main():
     solve_ms = sum(e[1].elapsed_time(e[2]) for e in ev) / K
     finite = bool(torch.isfinite(st.current("psi", 1)).all().item())
 
+    # multi-GPU: the two collectives of a step timed in isolation, then the same K steps with
+    # the halo / interior overlap toggled (all ranks take part in both)
+    comm, overlap_ab = None, None
+    if args.comm_probe_reps > 0 and (world > 1 or args.comm_self) and args.solver == "spectral":
+        comm = st.comm_probe(args.comm_probe_reps)
+        if dist is not None:
+            cv = torch.tensor([comm["halo_ms"], comm["allgather_ms"]], dtype=torch.float64,
+                              device="cuda" if args.transport == "rccl" else "cpu")
+            dist.all_reduce(cv, op=dist.ReduceOp.MAX)
+            comm["halo_ms_max_over_ranks"], comm["allgather_ms_max_over_ranks"] = float(cv[0]), float(cv[1])
+        comm["share_of_step"] = (comm.get("halo_ms_max_over_ranks", comm["halo_ms"])
+                                 + comm.get("allgather_ms_max_over_ranks", comm["allgather_ms"])) / (el * 1e3 / K)
+        st.set_overlap(not args.overlap)
+        for _ in range(3):
+            st.step(t)
+            t += 1
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        st.run(t, K)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el2 = time.perf_counter() - t1
+        t += K
+        if dist is not None:
+            tt = torch.tensor([el2], dtype=torch.float64, device="cuda" if args.transport == "rccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el2 = float(tt.item())
+        st.set_overlap(args.overlap)
+        overlap_ab = {"halo_overlap": not args.overlap, "value": world * K / el2, "ms_per_step": el2 * 1e3 / K,
+                      "steps": K, "note": "the same K steps re-timed in this invocation with qg_set_overlap "
+                                          "toggled (the headline value uses halo_overlap of config)"}
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -366,10 +477,22 @@ def main():
     }
     if pcg is not None:
         out["pcg_solver"] = pcg
+    if comm is not None:
+        out["comm"] = comm
+    if overlap_ab is not None:
+        out["overlap_ab"] = overlap_ab
+    if args.dropin_steps > 0 and world == 1 and args.solver == "spectral" and args.dtype == "f64" \
+            and not args.comm_self:
+        del st
+        torch.cuda.empty_cache()
+        d = dropin_variant(qgamd, m, n, 3, args.dropin_steps, torch)
+        d["vs_qg_run_step"] = d["ms_per_step"] / ms
+        out["dropin"] = d
     if args.cpu_steps > 0 and world == 1 and args.dtype == "f64":
         out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads, args.cpu_steps_1t)
     else:
         out["cpu_baseline"] = None
+    validate_record(out)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define QG_ABI_VERSION 3
+#define QG_ABI_VERSION 4
 
 typedef enum {
     QG_OK = 0,
@@ -142,6 +142,14 @@ int qg_run(qg_ctx *ctx, int64_t first_step, int64_t nsteps); /* loop run_model_n
 int qg_slot(const qg_ctx *ctx, int which, int logical, int *physical);
 int qg_set_slots(qg_ctx *ctx, const int heads[3]); /* restore a saved rotation (resume)  */
 int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2,3       */
+/* store_new_state! semantics (model.jl:102-106) on every call: slot 1 holds the newest
+ * values after each qg_evolve_zeta / qg_evolve_psi, as the reference's copies leave them.
+ * The history is shifted in place (slot 3 <- 2 <- 1: two slot copies per field, the
+ * reference's own data movement) before the new values are written to slot 1, so the heads
+ * stay 0 and no qg_canonicalize is needed.  on = 1 canonicalizes first.  For callers that
+ * hand the reference's arrays to every call (evolve_zeta!(model, zeta, psi, t, f_store));
+ * qg_run is faster rotating (the default, on = 0).                                          */
+int qg_set_keep_order(qg_ctx *ctx, int on);
 int qg_get_stats(qg_ctx *ctx, qg_stats *out);
 /* PCG with the spectral preconditioner and an invertible P_fwd (the default) takes the
  * certified step: psi = the spectral solve, accepted when the 5-point residual satisfies
@@ -228,6 +236,12 @@ int qg_comm_set_timeout(qg_ctx *ctx, double seconds);
  * geometry).  Default: the environment variable QG_OVERLAP (read at qg_create), else 0.
  * No effect on a single GPU (no exchange) or for P < 8 (no interior worth splitting).   */
 int qg_set_overlap(qg_ctx *ctx, int on);
+/* Time the two collectives of a multi-GPU step in isolation (HIP events on the context's
+ * stream, `reps` back-to-back calls each; every rank calls it): out[0] = ms per halo exchange
+ * (pack + grouped send/recv of the depth-2 rows of psi and zeta), out[1] = bytes this rank
+ * sends per exchange, out[2] = ms per record all-gather of the direct solve, out[3] = bytes
+ * this rank receives per all-gather.  Spectral solver only (QG_ERR_UNSUPPORTED for PCG).    */
+int qg_comm_probe(qg_ctx *ctx, int reps, double out[4]);
 /* The posting schedule of one halo exchange on `rank` of a ring of `nranks` y-slabs, as the
  * library issues it (RCCL: one ncclGroupStart/End; host transport: one sendrecv call):
  * sends k = 0, 1 go to send_peer[k] from buffer send_buf[k], receives k = 0, 1 come from

@@ -84,6 +84,18 @@ struct qg_ctx {
     hipEvent_t pace_ev = nullptr;  // multi-GPU pacing (qg_step)
     bool pace_armed = false;
     int64_t pace_count = 0;
+    // qg_set_keep_order: every call leaves slot 1 = newest, as store_new_state! does
+    // (model.jl:102-106), by shifting the history slots in place before the new values are
+    // written; the heads then stay 0
+    bool keep_order = false;
+    bool capturing = false;  // a step graph is being captured (no host reads, no polls)
+    // deferred PCG: the latch is copied to page-locked memory every QG_PACE_STEPS steps and
+    // read one interval later without blocking, so a failed certificate stops qg_step /
+    // qg_run within a bounded number of steps
+    double *latch_host = nullptr;
+    hipEvent_t latch_ev = nullptr;
+    bool latch_armed = false;
+    int64_t poll_count = 0;
     double *wind = nullptr;  // [P] wind forcing of the local rows (qg_params.wind_tau0 != 0)
     double *diag = nullptr;  // diagnostics scratch: partial records | record | gathered records
     size_t diag_cap = 0;
@@ -243,12 +255,27 @@ int qg_destroy(qg_ctx *c) {
     if (c->gev_in) (void)hipEventDestroy(c->gev_in);
     if (c->gev_out) (void)hipEventDestroy(c->gev_out);
     if (c->pace_ev) (void)hipEventDestroy(c->pace_ev);
+    if (c->latch_ev) {
+        (void)hipEventSynchronize(c->latch_ev);
+        (void)hipEventDestroy(c->latch_ev);
+    }
+    if (c->latch_host) (void)hipHostFree(c->latch_host);
     delete c;
     return QG_OK;
 }
 
+// A deferred PCG certification still waiting for its tendency reads the (zeta, psi) slots of
+// its solve; anything that moves, replaces or overwrites those slots runs it first.
+static int settle_pcg(qg_ctx *c) {
+    if (!c->pcg || !c->pcg->pending()) return QG_OK;
+    QG_HIP(hipSetDevice(c->device));
+    return c->pcg->certify_pending(c->stream, c->distributed ? comm_allgather : nullptr, c->comm);
+}
+
+// (the arrays bound before must still be valid here: a pending certification reads them)
 int qg_bind_state(qg_ctx *c, void *zeta, void *psi, void *f_store) {
     if (!c || !zeta || !psi || !f_store) return QG_ERR_INVALID_ARG;
+    if (c->zeta) QG_CHECK(settle_pcg(c));
     drop_graphs(c);
     c->zeta = zeta;
     c->psi = psi;
@@ -263,6 +290,7 @@ int qg_initialise(qg_ctx *c, uint64_t seed1, uint64_t seed2) {
     if (!c) return QG_ERR_INVALID_ARG;
     if (!c->zeta) return QG_ERR_NOT_BOUND;
     const qg_params &p = c->p;
+    QG_CHECK(settle_pcg(c));
     QG_HIP(hipSetDevice(c->device));
     const double amp = p.initial_kick * p.U * p.Ly;
     QG_CHECK(launch_initialise_global(c->zeta, c->psi, c->fst, (int)c->esize, p.M, p.P, p.P * c->nranks,
@@ -285,6 +313,8 @@ int qg_set_slots(qg_ctx *c, const int heads[3]) {
     if (!c || !heads) return QG_ERR_INVALID_ARG;
     for (int k = 0; k < 3; ++k)
         if (heads[k] < 0 || heads[k] > 2) return QG_ERR_INVALID_ARG;
+    if (c->keep_order && (heads[0] || heads[1] || heads[2])) return QG_ERR_INVALID_ARG;
+    QG_CHECK(settle_pcg(c));
     for (int k = 0; k < 3; ++k) c->heads[k] = heads[k];
     return QG_OK;
 }
@@ -329,8 +359,21 @@ extern "C++" {
 template <class T>
 static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     const qg_params &p = c->p;
-    const int zh = c->heads[0], ph = c->heads[1], fh = c->heads[2];
-    const int zn = (zh + 2) % 3, fn = (fh + 2) % 3;
+    // physical slots read (zeta, psi, F(t-1), F(t-2)) and written (zeta, F).  Rotating: the
+    // new values go to the oldest slot and the heads move.  keep_order: the history is first
+    // shifted in place (slot 3 <- 2 <- 1, as store_new_state! copies), so the inputs are read
+    // from slots 2 and 3 and the new values are written to slot 1; the heads stay 0.
+    int zh = c->heads[0], fh = c->heads[2], fh2 = (fh + 1) % 3;
+    const int ph = c->heads[1];
+    int zn = (zh + 2) % 3, fn = (fh + 2) % 3;
+    if (c->keep_order) {
+        void *arr[2] = {c->zeta, c->fst};
+        QG_CHECK(launch_slot_shift(arr, 2, 2 * c->esize * c->F, c->stream));
+        zh = 1;
+        fh = 1;
+        fh2 = 2;
+        zn = fn = 0;
+    }
     TendArgsT<T> a{};
     a.M = p.M;
     a.P = p.P;
@@ -352,7 +395,7 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
         a.zeta[l] = c->fieldt<T>(c->zeta, l, zh);
         a.psi[l] = c->fieldt<T>(c->psi, l, ph);
         a.fprev1[l] = c->fieldt<T>(c->fst, l, fh);
-        a.fprev2[l] = c->fieldt<T>(c->fst, l, (fh + 1) % 3);
+        a.fprev2[l] = c->fieldt<T>(c->fst, l, fh2);
         a.zeta_out[l] = c->fieldt<T>(c->zeta, l, zn);
         a.f_out[l] = c->fieldt<T>(c->fst, l, fn);
     }
@@ -439,7 +482,13 @@ int qg_evolve_psi(qg_ctx *c) {
     if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
     if (!c->spec && !c->pcg) return QG_ERR_UNSUPPORTED;
     QG_HIP(hipSetDevice(c->device));
-    const int zh = c->heads[0], pn = (c->heads[1] + 2) % 3;
+    const int zh = c->heads[0];
+    int pn = (c->heads[1] + 2) % 3;
+    if (c->keep_order) {  // store_new_state!'s shift of psi, then the solve writes slot 1
+        void *arr[1] = {c->psi};
+        QG_CHECK(launch_slot_shift(arr, 1, 2 * c->esize * c->F, c->stream));
+        pn = 0;
+    }
     double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);  // (element type p.dtype)
     const double *z1 = c->field(c->zeta, 0, zh), *z2 = c->field(c->zeta, 1, zh);
     if (c->pcg) {
@@ -470,11 +519,54 @@ static int pace(qg_ctx *c) {
     return QG_OK;
 }
 
+// Deferred PCG: report new certification failures the device has latched.  Non-blocking
+// (wait = false): every QG_PACE_STEPS steps, read the copy of the latch made one interval
+// earlier if it has landed, then start a new copy.  Blocking (wait = true, the end of qg_run):
+// settle the pending check and read the latch now.
+static int poll_pcg(qg_ctx *c, bool wait) {
+    if (!c->pcg || !c->pcg->deferred() || c->capturing) return QG_OK;
+    if (!c->latch_host) {
+        QG_HIP(hipHostMalloc((void **)&c->latch_host, sizeof(double) * 8, hipHostMallocDefault));
+        QG_HIP(hipEventCreateWithFlags(&c->latch_ev, hipEventDisableTiming));
+    }
+    auto report = [&]() -> int {
+        const int64_t f = (int64_t)c->latch_host[1];
+        if (f > c->cert_reported) {
+            c->cert_reported = f;
+            return QG_ERR_NOT_CONVERGED;
+        }
+        return QG_OK;
+    };
+    if (wait) {
+        QG_CHECK(settle_pcg(c));
+        if (c->latch_armed) QG_CHECK(comm_wait(c->distributed ? c->comm : nullptr, c->stream, c->latch_ev,
+                                               "qg_run (PCG latch)"));
+        QG_HIP(hipMemcpyAsync(c->latch_host, c->pcg->latch(), sizeof(double) * 8, hipMemcpyDeviceToHost, c->stream));
+        QG_HIP(hipEventRecord(c->latch_ev, c->stream));
+        QG_CHECK(comm_wait(c->distributed ? c->comm : nullptr, c->stream, c->latch_ev, "qg_run (PCG latch)"));
+        c->latch_armed = false;
+        return report();
+    }
+    if (++c->poll_count % QG_PACE_STEPS != 0) return QG_OK;
+    if (c->latch_armed) {
+        const hipError_t q = hipEventQuery(c->latch_ev);
+        if (q == hipErrorNotReady) return QG_OK;  // the last copy is still in flight
+        QG_HIP(q);
+        c->latch_armed = false;
+        QG_CHECK(report());
+    }
+    QG_HIP(hipMemcpyAsync(c->latch_host, c->pcg->latch(), sizeof(double) * 8, hipMemcpyDeviceToHost, c->stream));
+    QG_HIP(hipEventRecord(c->latch_ev, c->stream));
+    c->latch_armed = true;
+    return QG_OK;
+}
+
 int qg_step(qg_ctx *c, int64_t timestep) {
     QG_CHECK(qg_evolve_zeta(c, timestep));
     const int st = qg_evolve_psi(c);
     if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
     QG_CHECK(pace(c));
+    QG_CHECK(poll_pcg(c, false));
     return st;
 }
 
@@ -505,6 +597,7 @@ static int step_graph(qg_ctx *c, hipGraphExec_t *out) {
     std::memcpy(heads0, c->heads, sizeof(heads0));
     hipStream_t saved = c->stream;
     c->stream = c->gstream;
+    c->capturing = true;
     hipGraph_t graph = nullptr;
     int st = hipStreamBeginCapture(c->gstream, hipStreamCaptureModeThreadLocal) == hipSuccess ? QG_OK : QG_ERR_HIP;
     if (st == QG_OK) {
@@ -512,6 +605,7 @@ static int step_graph(qg_ctx *c, hipGraphExec_t *out) {
         if (hipStreamEndCapture(c->gstream, &graph) != hipSuccess) st = QG_ERR_HIP;
     }
     c->stream = saved;
+    c->capturing = false;
     std::memcpy(c->heads, heads0, sizeof(heads0));  // (three steps: the rotation is back anyway)
     hipGraphExec_t exec = nullptr;
     if (st == QG_OK && hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) st = QG_ERR_HIP;
@@ -533,7 +627,11 @@ int qg_run(qg_ctx *c, int64_t first_step, int64_t nsteps) {
     int64_t t = first_step;
     const int64_t end = first_step + nsteps;
     for (; t < end && t < 3; ++t) QG_CHECK(qg_step(c, t));  // the Euler steps
-    if (end - t >= 6 && graphs_enabled(c) && c->initialised && c->zeta) {
+    // deferred PCG: a captured graph's first tendency certifies the solve before it only if
+    // that check was pending at capture; capture and replay only in that steady state (one
+    // stream step first when a standalone check has already settled it)
+    if (end - t >= 7 && graphs_enabled(c) && c->pcg && !c->pcg->pending()) QG_CHECK(qg_step(c, t++));
+    if (end - t >= 6 && graphs_enabled(c) && c->initialised && c->zeta && (!c->pcg || c->pcg->pending())) {
         QG_HIP(hipSetDevice(c->device));
         hipGraphExec_t g = nullptr;
         if (step_graph(c, &g) == QG_OK) {
@@ -547,7 +645,7 @@ int qg_run(qg_ctx *c, int64_t first_step, int64_t nsteps) {
         }
     }
     for (; t < end; ++t) QG_CHECK(qg_step(c, t));
-    return QG_OK;
+    return poll_pcg(c, true);  // deferred PCG: a failed certificate is reported by the run
 }
 
 int qg_canonicalize(qg_ctx *c) {
@@ -555,22 +653,28 @@ int qg_canonicalize(qg_ctx *c) {
     if (!c->zeta) return QG_ERR_NOT_BOUND;
     QG_HIP(hipSetDevice(c->device));
     QG_CHECK(flush_ghosts(c));  // pending ghost-ring refreshes
+    QG_CHECK(settle_pcg(c));    // (its check reads the slots about to move)
+    // one launch rotates every field whose newest slot is not physical 0: new slot q <- old
+    // slot (head + q) mod 3, each slot read once and written once, in place
+    void *arr[3];
+    int src[3][3], n = 0;
     void *bases[3] = {c->zeta, c->psi, c->fst};
-    char *tmp = nullptr;
-    const size_t fb = c->esize * c->F, bytes = fb * 6;
     for (int w = 0; w < 3; ++w) {
         if (c->heads[w] == 0) continue;
-        if (!tmp) QG_HIP(hipMallocAsync((void **)&tmp, bytes, c->stream));
-        QG_HIP(hipMemcpyAsync(tmp, bases[w], bytes, hipMemcpyDeviceToDevice, c->stream));
-        for (int logical = 1; logical <= 3; ++logical) {
-            const int phys = (c->heads[w] + logical - 1) % 3;
-            for (int l = 0; l < 2; ++l)
-                QG_HIP(hipMemcpyAsync(c->fieldv(bases[w], l, logical - 1), tmp + fb * (size_t)(l + 2 * phys), fb,
-                                      hipMemcpyDeviceToDevice, c->stream));
-        }
-        c->heads[w] = 0;
+        arr[n] = bases[w];
+        for (int q = 0; q < 3; ++q) src[n][q] = (c->heads[w] + q) % 3;
+        ++n;
     }
-    if (tmp) QG_HIP(hipFreeAsync(tmp, c->stream));
+    if (n) QG_CHECK(launch_slot_move(arr, src, n, 2 * c->esize * c->F, c->stream));
+    c->heads[0] = c->heads[1] = c->heads[2] = 0;
+    return QG_OK;
+}
+
+int qg_set_keep_order(qg_ctx *c, int on) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    if (on && !c->keep_order && c->zeta) QG_CHECK(qg_canonicalize(c));
+    if (c->keep_order != (on != 0)) drop_graphs(c);
+    c->keep_order = on != 0;
     return QG_OK;
 }
 
@@ -768,11 +872,14 @@ int qg_comm_unique_id(char out[128]) {
     return comm_unique_id(out);
 }
 
+// a state seeded by qg_initialise for another slab layout holds noise drawn for the wrong
+// global rows: refuse instead of stepping it (re-run qg_initialise after attaching).  Checked
+// before a communicator is created, so a refused attach leaves the context as it was.
+static bool seeded_for_other_slab(const qg_ctx *c, int nranks, int rank) {
+    return c->initialised && c->seeded_nranks > 0 && (c->seeded_nranks != nranks || c->seeded_rank != rank);
+}
+
 static int comm_attach(qg_ctx *c, int nranks, int rank) {
-    // a state seeded by qg_initialise for another slab layout holds noise drawn for the wrong
-    // global rows: refuse instead of stepping it (re-run qg_initialise after attaching)
-    if (c->initialised && c->seeded_nranks > 0 && (c->seeded_nranks != nranks || c->seeded_rank != rank))
-        return QG_ERR_INVALID_ARG;
     c->rank = rank;
     c->nranks = nranks;
     if (c->wind) {  // the slab's global rows changed
@@ -786,6 +893,8 @@ static int comm_attach(qg_ctx *c, int nranks, int rank) {
 
 int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return QG_ERR_INVALID_ARG;
+    if (seeded_for_other_slab(c, nranks, rank)) return QG_ERR_INVALID_ARG;
+    QG_CHECK(settle_pcg(c));  // (the solver is rebuilt)
     QG_HIP(hipSetDevice(c->device));
     if (c->comm) {
         comm_destroy(c->comm);
@@ -798,6 +907,8 @@ int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
 int qg_comm_init_host(qg_ctx *c, int nranks, int rank, qg_allgather_fn allgather, qg_sendrecv_fn sendrecv,
                       void *user) {
     if (!c || nranks < 1 || rank < 0 || rank >= nranks || !allgather || !sendrecv) return QG_ERR_INVALID_ARG;
+    if (seeded_for_other_slab(c, nranks, rank)) return QG_ERR_INVALID_ARG;
+    QG_CHECK(settle_pcg(c));  // (the solver is rebuilt)
     QG_HIP(hipSetDevice(c->device));
     if (c->comm) {
         comm_destroy(c->comm);
@@ -805,6 +916,51 @@ int qg_comm_init_host(qg_ctx *c, int nranks, int rank, qg_allgather_fn allgather
     }
     QG_CHECK(comm_init_host(&c->comm, nranks, rank, allgather, sendrecv, user));
     return comm_attach(c, nranks, rank);
+}
+
+// Time the step's two collectives in isolation on the context's stream (HIP events around
+// `reps` back-to-back calls each): the tendency's halo exchange (pack + grouped send/recv of
+// the depth-2 rows of psi and zeta, both layers, exactly as a step posts it) and the solve's
+// record all-gather.  out[0] halo ms per exchange, out[1] bytes this rank sends per exchange,
+// out[2] all-gather ms, out[3] bytes this rank receives per all-gather.  Every rank must call
+// it (collectives).  Harmless to the state: the halo rows it receives are the ones the next
+// step receives again, and the gathered records are recomputed by the next solve.
+int qg_comm_probe(qg_ctx *c, int reps, double out[4]) {
+    if (!c || !out || reps < 1) return QG_ERR_INVALID_ARG;
+    if (!c->distributed || !c->comm) return QG_ERR_RCCL;
+    if (!c->spec) return QG_ERR_UNSUPPORTED;
+    QG_HIP(hipSetDevice(c->device));
+    const qg_params &p = c->p;
+    const int zh = c->heads[0], ph = c->heads[1];
+    double *f2[4] = {c->field(c->psi, 0, ph), c->field(c->psi, 1, ph), c->field(c->zeta, 0, zh),
+                     c->field(c->zeta, 1, zh)};
+    const double *hr[16];
+    const SpecArgs &sa = c->spec->args();
+    hipEvent_t ev[3];
+    for (auto &e : ev) QG_HIP(hipEventCreate(&e));
+    int st = QG_OK;
+    auto run = [&]() -> int {
+        QG_CHECK(comm_halo_rows(c->comm, f2, 4, c->row_words(), p.P, c->stream, hr));  // (warm)
+        QG_CHECK(comm_allgather(c->comm, sa.rec, c->spec->gather_buf(), sa.rec_stride, c->stream));
+        QG_HIP(hipEventRecord(ev[0], c->stream));
+        for (int k = 0; k < reps; ++k) QG_CHECK(comm_halo_rows(c->comm, f2, 4, c->row_words(), p.P, c->stream, hr));
+        QG_HIP(hipEventRecord(ev[1], c->stream));
+        for (int k = 0; k < reps; ++k)
+            QG_CHECK(comm_allgather(c->comm, sa.rec, c->spec->gather_buf(), sa.rec_stride, c->stream));
+        QG_HIP(hipEventRecord(ev[2], c->stream));
+        QG_CHECK(comm_wait(c->comm, c->stream, ev[2], "qg_comm_probe"));
+        float a = 0, b = 0;
+        QG_HIP(hipEventElapsedTime(&a, ev[0], ev[1]));
+        QG_HIP(hipEventElapsedTime(&b, ev[1], ev[2]));
+        out[0] = a / reps;
+        out[1] = 2.0 * 8 * (double)c->row_words() * 8;  // two messages of 8 rows (2 x 4 fields)
+        out[2] = b / reps;
+        out[3] = (double)sa.rec_stride * 8 * (c->nranks - 1);
+        return QG_OK;
+    };
+    st = run();
+    for (auto &e : ev) (void)hipEventDestroy(e);
+    return st;
 }
 
 // ---- solver handles ---------------------------------------------------------------------

@@ -220,6 +220,14 @@ int launch_arakawa(const double *z, const double *p, double *out, int64_t M, int
                    hipStream_t s);
 int launch_fill_ghosts(double *b, int64_t M, int64_t P, hipStream_t s);
 int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s);
+// in-place slot moves of (M+2, P+2, 2, 3) arrays: new slot q <- old slot src[k][q] (-1: kept)
+// (slot_bytes = bytes of one slot, both layers; a multiple of 16)
+int launch_slot_move(void *const *arrays, const int (*src)[3], int narrays, size_t slot_bytes, hipStream_t s);
+// store_new_state!'s shift (slot 3 <- slot 2 <- slot 1) of n arrays
+inline int launch_slot_shift(void *const *arrays, int narrays, size_t slot_bytes, hipStream_t s) {
+    static const int sh[3][3] = {{-1, 0, 1}, {-1, 0, 1}, {-1, 0, 1}};
+    return launch_slot_move(arrays, sh, narrays, slot_bytes, s);
+}
 // esize = sizeof(element) of the state fields (8 or 4)
 int launch_initialise_global(void *zeta, void *psi, void *f_store, int esize, int64_t M, int64_t P,
                              int64_t P_total, int64_t j_offset, double amp, double S1, double S2,

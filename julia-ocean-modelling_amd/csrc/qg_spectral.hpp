@@ -98,6 +98,7 @@ public:
               const double *pin_out = nullptr);  // optional per-call projections
     const SpecArgs &args() const { return a_; }
     size_t device_bytes() const { return bytes_; }
+    double *gather_buf() const { return grec_buf_; }  // the record all-gather's target
 
 private:
     SpecArgs a_{};

@@ -696,6 +696,73 @@ __global__ void initialise_kernel(T *zeta, T *psi, int64_t M, int64_t P, int64_t
 }
 
 // ------------------------------------------------------------------------------------
+// Slot moves of up to three (M+2, P+2, 2, 3) history arrays in one launch (blockIdx.y =
+// array), in place: new slot s <- old slot src[s] (-1: slot s is left alone).  Slots are
+// contiguous blocks of `n16` 16-byte vectors (2 layers x (M+2)(P+2) elements: a multiple of
+// 16 B for F64, and for F32 since M is even).  Each element's sources are read into
+// registers before any of its destinations is written, by the same thread, so any
+// permutation of the three slots is safe.  Two uses:
+//   store_new_state!'s shift (model.jl:102-106: X[:,:,:,3] .= X[:,:,:,2]; X[:,:,:,2] .=
+//     X[:,:,:,1]): src = {-1, 0, 1}, 2 reads + 2 writes per element, slot 1 left for the
+//     new values;
+//   qg_canonicalize's rotation of a field whose newest slot is physical h: src = {h, h+1,
+//     h+2} mod 3, each slot read once and written once.
+// ------------------------------------------------------------------------------------
+struct SlotMoveArgs {
+    uint4 *base[3];
+    int src[3][3];
+    int64_t n16;
+};
+
+constexpr int SLOT_MOVE_V = 4;  // vectors per thread and slot: all loads in flight before the stores
+
+__global__ __launch_bounds__(256) void slot_move_kernel(SlotMoveArgs a) {
+    const int k = blockIdx.y;
+    uint4 *b = a.base[k];
+    const int s0 = a.src[k][0], s1 = a.src[k][1], s2 = a.src[k][2];
+    const int64_t n = a.n16;
+    const int64_t i0 = (int64_t)blockIdx.x * (256 * SLOT_MOVE_V) + threadIdx.x;
+    uint4 v[3][SLOT_MOVE_V];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+        if (s0 == q || s1 == q || s2 == q) {
+#pragma unroll
+            for (int u = 0; u < SLOT_MOVE_V; ++u) {
+                const int64_t i = i0 + u * 256;
+                if (i < n) v[q][u] = b[q * n + i];
+            }
+        }
+#pragma unroll
+    for (int u = 0; u < SLOT_MOVE_V; ++u) {
+        const int64_t i = i0 + u * 256;
+        if (i < n) {
+            if (s0 >= 0) b[i] = v[s0][u];
+            if (s1 >= 0) b[n + i] = v[s1][u];
+            if (s2 >= 0) b[2 * n + i] = v[s2][u];
+        }
+    }
+}
+
+int launch_slot_move(void *const *arrays, const int (*src)[3], int narrays, size_t slot_bytes, hipStream_t s) {
+    if (narrays < 1 || narrays > 3 || slot_bytes % 16 != 0) return QG_ERR_INVALID_ARG;
+    SlotMoveArgs a{};
+    for (int k = 0; k < narrays; ++k) {
+        if (reinterpret_cast<uintptr_t>(arrays[k]) % 16 != 0) return QG_ERR_INVALID_ARG;
+        a.base[k] = static_cast<uint4 *>(arrays[k]);
+        for (int q = 0; q < 3; ++q) {
+            if (src[k][q] < -1 || src[k][q] > 2) return QG_ERR_INVALID_ARG;
+            a.src[k][q] = src[k][q];
+        }
+    }
+    a.n16 = (int64_t)(slot_bytes / 16);
+    const int64_t gx = (a.n16 + 256 * SLOT_MOVE_V - 1) / (256 * SLOT_MOVE_V);
+    if (gx > 0x7fffffff) return QG_ERR_UNSUPPORTED;
+    slot_move_kernel<<<dim3((unsigned)std::max<int64_t>(gx, 1), (unsigned)narrays), 256, 0, s>>>(a);
+    QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+// ------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------
 static dim3 grid_rows(int64_t M, int64_t P, int bs) { return dim3((unsigned)((M + bs - 1) / bs), (unsigned)P); }

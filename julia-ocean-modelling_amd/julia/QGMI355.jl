@@ -97,7 +97,9 @@ mutable struct QGState{T<:Union{Float64,Float32}}
     zeta::ROCArray{T,4}
     psi::ROCArray{T,4}
     f_store::ROCArray{T,4}
+    model::Any  # the model the context was created for (the reference-signature cache checks it)
 end
+QGState{T}(ctx, zeta, psi, f_store) where {T} = QGState{T}(ctx, zeta, psi, f_store, nothing)
 
 function QGState(model; P_local::Integer=model.P, dtype::Type=Float64, kw...)
     params = Ref(QGParams(model; P_local=P_local, dtype=dtype, kw...))
@@ -139,33 +141,52 @@ evolve_psi!(model, s::QGState, poisson=nothing, helmholtz=nothing) =
 # then `evolve_psi!(model, zeta, psi, P, H)`) on device arrays gets a library context bound to
 # those arrays, created on first use and cached by the arrays' addresses.  Each call leaves
 # the arrays in the reference's slot order (slot 1 = newest), as store_new_state! does, so
-# `zeta[:, :, 1, 1]` means what it means in the reference.  (The rotation-free fast path is
-# QGState / run_model_no_output.)
+# `zeta[:, :, 1, 1]` means what it means in the reference: the context keeps that order on
+# the device (qg_set_keep_order: the history shifted in place before each new value, two
+# slot copies per field, the reference's own data movement).  (The rotation-free fast path
+# is QGState / run_model_no_output.)
 const _BOUND = Dict{NTuple{3,UInt},QGState}()
 
 function _bound_state(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, f_store::ROCArray{T,4}) where {T}
     size(zeta) == size(psi) == size(f_store) == (model.M + 2, model.P + 2, 2, 3) ||
         throw(DimensionMismatch("zeta, psi, f_store must be (M+2, P+2, 2, 3)"))
     key = (UInt(pointer(zeta)), UInt(pointer(psi)), UInt(pointer(f_store)))
-    get!(_BOUND, key) do
-        params = Ref(QGParams(model; dtype=T))
-        ctx = Ref{Ptr{Cvoid}}(C_NULL)
-        @qgcheck qg_create ccall((:qg_create, libqg), Cint, (Ptr{QGParams}, Cint, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
-                                 params, AMDGPU.device_id(AMDGPU.device()) - 1, stream_ptr(), ctx)
-        @qgcheck qg_bind_state ccall((:qg_bind_state, libqg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
-                                     ctx[], pointer(zeta), pointer(psi), pointer(f_store))
-        s = QGState{T}(ctx[], zeta, psi, f_store)
-        finalizer(x -> ccall((:qg_destroy, libqg), Cint, (Ptr{Cvoid},), x.ctx), s)
-        s
+    s = get(_BOUND, key, nothing)
+    s !== nothing && s.model == model && return s
+    s === nothing || unbind!(zeta, psi, f_store)  # a different model for these arrays
+    params = Ref(QGParams(model; dtype=T))
+    ctx = Ref{Ptr{Cvoid}}(C_NULL)
+    @qgcheck qg_create ccall((:qg_create, libqg), Cint, (Ptr{QGParams}, Cint, Ptr{Cvoid}, Ptr{Ptr{Cvoid}}),
+                             params, AMDGPU.device_id(AMDGPU.device()) - 1, stream_ptr(), ctx)
+    @qgcheck qg_bind_state ccall((:qg_bind_state, libqg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
+                                 ctx[], pointer(zeta), pointer(psi), pointer(f_store))
+    @qgcheck qg_set_keep_order ccall((:qg_set_keep_order, libqg), Cint, (Ptr{Cvoid}, Cint), ctx[], 1)
+    s = QGState{T}(ctx[], zeta, psi, f_store, model)
+    finalizer(x -> ccall((:qg_destroy, libqg), Cint, (Ptr{Cvoid},), x.ctx), s)
+    _BOUND[key] = s
+end
+
+"""`unbind!(zeta, psi, f_store)` / `unbind!()`: release the cached context of the
+reference-signature calls bound to these arrays (or all of them); the cache holds the arrays,
+so without this they stay alive.  Returns the number released."""
+function unbind!(zeta=nothing, psi=nothing, f_store=nothing)
+    keys_ = zeta === nothing ? collect(keys(_BOUND)) :
+            [k for k in keys(_BOUND) if k[1] == UInt(pointer(zeta)) &&
+             (psi === nothing || k[2] == UInt(pointer(psi))) &&
+             (f_store === nothing || k[3] == UInt(pointer(f_store)))]
+    for k in keys_
+        s = pop!(_BOUND, k)
+        @qgcheck qg_synchronize ccall((:qg_synchronize, libqg), Cint, (Ptr{Cvoid},), s.ctx)
+        finalize(s)
     end
+    length(keys_)
 end
 
 """`evolve_zeta!(model, zeta, psi, timestep, f_store)` — model.jl:155 with its signature."""
 function evolve_zeta!(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, timestep::Integer,
                       f_store::ROCArray{T,4}) where {T<:Union{Float64,Float32}}
     s = _bound_state(model, zeta, psi, f_store)
-    evolve_zeta!(model, s, timestep)
-    canonical!(s)
+    evolve_zeta!(model, s, timestep)  # (keep-order context: the arrays stay in reference order)
     nothing
 end
 
@@ -177,8 +198,9 @@ function evolve_psi!(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, poisson=not
     isempty(key_match) && throw(ArgumentError("evolve_psi!: call evolve_zeta! on these arrays first " *
                                               "(it binds them with their f_store)"))
     s = only(key_match)
+    s.model == model || throw(ArgumentError("evolve_psi!: these arrays are bound to a different model " *
+                                            "(call evolve_zeta! with this model first, or unbind! them)"))
     evolve_psi!(model, s)
-    canonical!(s)
     nothing
 end
 

@@ -75,6 +75,7 @@ SIGNATURES = [
     ("qg_slot", C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(C.c_int)]),
     ("qg_set_slots", C.c_int, [_vp, C.c_int * 3]),
     ("qg_canonicalize", C.c_int, [_vp]),
+    ("qg_set_keep_order", C.c_int, [_vp, C.c_int]),
     ("qg_get_stats", C.c_int, [_vp, C.POINTER(QgStats)]),
     ("qg_solver_stats", C.c_int, [_vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
                                   C.POINTER(C.c_double)]),
@@ -87,6 +88,7 @@ SIGNATURES = [
     ("qg_comm_init_host", C.c_int, [_vp, C.c_int, C.c_int, AllgatherFn, SendrecvFn, _vp]),
     ("qg_comm_set_timeout", C.c_int, [_vp, C.c_double]),
     ("qg_set_overlap", C.c_int, [_vp, C.c_int]),
+    ("qg_comm_probe", C.c_int, [_vp, C.c_int, C.POINTER(C.c_double)]),
     ("qg_set_pcg_sync", C.c_int, [_vp, C.c_int]),
     ("qg_pcg_certificate", C.c_int, [_vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                      C.POINTER(C.c_double)]),

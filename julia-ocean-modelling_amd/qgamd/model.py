@@ -248,6 +248,14 @@ class State:
         interior rows' tendency meanwhile (multi-rank only; bit-identical results)."""
         call("qg_set_overlap", self._ctx, 1 if on else 0)
 
+    def comm_probe(self, reps=20):
+        """qg_comm_probe: event-timed halo exchange and record all-gather of one step, in
+        isolation (every rank must call it): ms and bytes per collective."""
+        out = (C.c_double * 4)()
+        call("qg_comm_probe", self._ctx, int(reps), out)
+        return {"halo_ms": out[0], "halo_bytes_sent": int(out[1]), "allgather_ms": out[2],
+                "allgather_bytes_received": int(out[3]), "reps": int(reps)}
+
     def set_pcg_sync(self, sync=True):
         """qg_set_pcg_sync: 1 = the host checks every PCG residual (and iterates when the
         certificate fails); 0 = deferred on-device certification (default)."""
@@ -330,6 +338,12 @@ class State:
     def canonicalize(self):
         call("qg_canonicalize", self._ctx)
 
+    def set_keep_order(self, on=True):
+        """qg_set_keep_order: every call leaves slot 1 = newest (store_new_state!'s shift, in
+        place, before the new values are written), so the arrays are always in the
+        reference's slot order; off (default) rotates the slots instead."""
+        call("qg_set_keep_order", self._ctx, 1 if on else 0)
+
     def to_numpy(self, which):
         """Reference-ordered numpy array of shape (M+2, P+2, 2, 3) (Julia index order).
         Synchronises first (multi-GPU: completes the lazily refreshed ghost rows)."""
@@ -352,12 +366,34 @@ _BOUND = {}
 
 def _bound_state(m, zeta, psi, f_store):
     """The library context bound to a caller's (zeta, psi, f_store) arrays, created on first
-    use and cached by their addresses (the reference-signature calls below)."""
+    use and cached by their addresses (the reference-signature calls below).  The context
+    keeps the reference's slot order on every call (qg_set_keep_order), as store_new_state!
+    does.  A different model for the same arrays replaces the cached context."""
     key = (zeta.data_ptr(), psi.data_ptr(), f_store.data_ptr())
     st = _BOUND.get(key)
     if st is None or st.model != m:
+        if st is not None:
+            st.synchronize()  # settle the old context's pending work on these arrays
         st = _BOUND[key] = State(m, device=zeta.device, dtype=zeta.dtype, arrays=(zeta, psi, f_store))
+        st.set_keep_order(True)
     return st
+
+
+def unbind(zeta=None, psi=None, f_store=None):
+    """Release the cached contexts of the reference-signature calls: the one bound to these
+    arrays, or all of them (no arguments).  The contexts hold references to the arrays, so
+    without this the arrays stay alive as long as the process."""
+    if zeta is None:
+        keys = list(_BOUND)
+    else:
+        keys = [k for k in _BOUND if k[0] == zeta.data_ptr()
+                and (psi is None or k[1] == psi.data_ptr())
+                and (f_store is None or k[2] == f_store.data_ptr())]
+    for k in keys:
+        st = _BOUND.pop(k)
+        st.synchronize()
+        del st
+    return len(keys)
 
 
 def evolve_zeta_(m, *args):
@@ -373,8 +409,7 @@ def evolve_zeta_(m, *args):
         return
     zeta, psi, timestep, f_store = args
     st = _bound_state(m, zeta, psi, f_store)
-    st.evolve_zeta_(timestep)
-    st.canonicalize()
+    st.evolve_zeta_(timestep)  # (keep-order context: the arrays stay in reference order)
 
 
 class SolverHandle:
@@ -401,22 +436,22 @@ def evolve_psi_(m, *args):
     bound by :func:`evolve_zeta_` (which knows their f_store)."""
     if isinstance(args[0], State):
         state, poisson, helmholtz = (tuple(args) + (None, None))[:3]
-        canonical = False
     else:
         zeta, psi, poisson, helmholtz = args
         hits = [st for k, st in _BOUND.items() if k[:2] == (zeta.data_ptr(), psi.data_ptr())]
         if len(hits) != 1:
             raise ValueError("evolve_psi_: call evolve_zeta_ on these arrays first (it binds them "
                              "with their f_store)")
-        state, canonical = hits[0], True
+        state = hits[0]
+        if state.model != m:
+            raise ValueError("evolve_psi_: these arrays are bound to a different model (call "
+                             "evolve_zeta_ with this model first, or unbind them)")
     for h, kind in ((poisson, "poisson"), (helmholtz, "helmholtz")):
         if h is not None and (h.kind != kind or h.M != m.M or h.P != m.P or h.dx != m.dx):
             raise ValueError(f"{kind} handle does not match the model")
     if helmholtz is not None and helmholtz.alpha != S_eig(m):
         raise ValueError("helmholtz handle alpha != S_eig(model)")
     state.evolve_psi_()
-    if canonical:
-        state.canonicalize()
 
 
 def run_model_no_output(m, nsteps=None, seeds=(SEED_LAYER1, SEED_LAYER2), **kw):

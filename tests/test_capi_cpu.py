@@ -37,7 +37,7 @@ def test_exports_every_declared_symbol(qglib):
 
 
 def test_abi_version_and_strerror(qglib):
-    assert qglib.qg_abi_version() == 3
+    assert qglib.qg_abi_version() == 4
     assert qglib.qg_strerror(0) == b"ok"
     assert b"unsupported" in qglib.qg_strerror(-2)
 

@@ -1,0 +1,155 @@
+"""The reference-signature drop-in path and the slot bookkeeping around it.
+
+- qg_set_keep_order: store_new_state! semantics (model.jl:102-106) on every call -- the
+  history shifted in place, slot 1 = newest -- must give exactly the rotating path's logical
+  arrays (bitwise), for both solvers and F32, stepping and qg_run.
+- qg_canonicalize: the in-place rotation of every slot (one launch, each slot read once and
+  written once) restores the reference order bitwise, and stepping on afterwards is unchanged.
+- Deferred PCG certification: a check still pending when the slots move
+  (canonicalize, set_slots, initialise, bind) is settled first and reports no false failure;
+  HIP-graph replay captures and replays only in the pending steady state, so every solve is
+  certified exactly once.
+"""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def qg():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+    return qgamd
+
+
+def _logical(st):
+    return {n: st.logical(n).clone() for n in ("zeta", "psi", "f_store")}
+
+
+def _physical(st):
+    return {"zeta": st.zeta.clone(), "psi": st.psi.clone(), "f_store": st.f_store.clone()}
+
+
+def _same(a, b):
+    import torch
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("M,P,solver,f32", [(64, 48, 0, False), (128, 128, 1, False), (64, 64, 0, True),
+                                            (45, 30, 0, False)])
+def test_keep_order_matches_rotation(qg, M, P, solver, f32):
+    import torch
+    m = qg.bench_model(M, P=P)
+    kw = dict(solver=solver, dtype=torch.float32 if f32 else None)
+    a = qg.initialise_model(m, **kw)
+    b = qg.initialise_model(m, **kw)
+    b.set_keep_order(True)
+    for t in range(1, 8):
+        a.step(t)
+        b.step(t)
+        assert b.heads() == [0, 0, 0]
+        _same(_physical(b), _logical(a))
+    a.run(8, 11)
+    b.run(8, 11)
+    _same(_physical(b), _logical(a))
+
+
+def test_keep_order_switch_canonicalizes(qg):
+    m = qg.bench_model(64, P=32)
+    a = qg.initialise_model(m)
+    a.run(1, 5)  # heads rotated
+    want = _logical(a)
+    assert a.heads() != [0, 0, 0]
+    a.set_keep_order(True)
+    assert a.heads() == [0, 0, 0]
+    _same(_physical(a), want)
+    with pytest.raises(qg.QGError):
+        a.set_heads([1, 0, 0])  # a rotation cannot be restored while the order is kept
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5])
+def test_canonicalize_in_place(qg, k):
+    m = qg.bench_model(64, P=40)
+    a = qg.initialise_model(m)
+    b = qg.initialise_model(m)
+    for t in range(1, k + 1):
+        a.step(t)
+        b.step(t)
+    want = _logical(a)
+    a.canonicalize()
+    assert a.heads() == [0, 0, 0]
+    _same(_physical(a), want)
+    for t in range(k + 1, k + 5):
+        a.step(t)
+        b.step(t)
+    _same(_logical(a), _logical(b))
+
+
+def test_pending_certificate_settled_before_slots_move(qg):
+    """a deferred check left pending by the last solve reads that solve's slots;
+    canonicalize / set_slots / initialise run it first, so no false failure is reported."""
+    m = qg.bench_model(64)
+    st = qg.initialise_model(m, solver=1)
+    for t in range(1, 5):
+        st.step(t)           # the 4th solve's check is pending (it rides in the next tendency)
+    st.canonicalize()        # moves psi slot 2 -> slot 0: settled first
+    st.synchronize()
+    c = st.pcg_certificate()
+    assert c["solves"] == 4 and c["failures"] == 0, c
+    st.step(5)
+    h = st.heads()
+    st.set_heads(h)          # settles the 5th solve's check
+    st.step(6)
+    st.initialise()          # settles the 6th, then overwrites the state
+    st.synchronize()
+    c = st.pcg_certificate()
+    assert c["solves"] == 6 and c["failures"] == 0, c
+
+
+def test_graph_replay_certifies_each_solve_once(qg, monkeypatch):
+    """replays only in the pending steady state.  A run that starts after a
+    standalone check settled the pending solve takes one stream step first; a cached graph
+    replayed after a settle does not re-check a solve.  Every solve certified exactly once,
+    states bitwise equal to stream launches."""
+    m = qg.bench_model(128)
+    ref = qg.initialise_model(m, solver=1)
+    ref.run(1, 30)
+    monkeypatch.setenv("QG_GRAPH", "1")
+    st = qg.initialise_model(m, solver=1)
+    st.run(1, 3)
+    assert st.pcg_certificate()["solves"] == 3   # (qg_run settles at its end)
+    st.run(4, 12)        # one stream step, then graph replays (captured with the check pending)
+    c = st.pcg_certificate()
+    assert c["solves"] == 15 and c["failures"] == 0, c
+    st.run(16, 15)       # the cached graphs, after a settle
+    c = st.pcg_certificate()
+    assert c["solves"] == 30 and c["failures"] == 0, c
+    _same(_logical(st), _logical(ref))
+
+
+@pytest.mark.parametrize("f32", [False, True])
+def test_reference_signatures_keep_order_and_unbind(qg, f32):
+    """evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(model, zeta, psi, P, H) on bare
+    arrays (an F32 state too): slot 1 newest after every call, equal to the
+    rotating State; a different model for the same arrays is refused by evolve_psi_; unbind
+    releases the cached context."""
+    import torch
+    m = qg.bench_model(64, P=48)
+    dt = torch.float32 if f32 else None
+    ref2 = qg.initialise_model(m, dtype=dt)
+    zeta, psi, f_store = ref2.zeta.clone(), ref2.psi.clone(), ref2.f_store.clone()
+    pc = qg.get_poisson_cholesky(m.M, m.P, m.dx)
+    hc = qg.get_helmholtz_cholesky(m.M, m.P, m.dx, qg.S_eig(m))
+    for t in range(1, 6):
+        qg.evolve_zeta_(m, zeta, psi, t, f_store)
+        qg.evolve_psi_(m, zeta, psi, pc, hc)
+        ref2.step(t)
+        _same({"zeta": zeta, "psi": psi, "f_store": f_store}, _logical(ref2))
+    m2 = qg.bench_model(64, P=48, dt=m.dt / 2)
+    with pytest.raises(ValueError):
+        qg.evolve_psi_(m2, zeta, psi, pc, hc)
+    assert qg.unbind(zeta, psi, f_store) == 1
+    assert qg.unbind(zeta, psi, f_store) == 0

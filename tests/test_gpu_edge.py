@@ -167,6 +167,12 @@ def test_attach_after_single_rank_seed_is_refused():
     noop_sr = _lib.SendrecvFn(lambda *a: 0)
     rc = _lib.lib().qg_comm_init_host(st._ctx, 2, 0, noop_ag, noop_sr, None)
     assert rc == _lib.QG_ERR_INVALID_ARG
+    # the refused attach left the context untouched (no communicator, not distributed): it
+    # still steps as the single-GPU periodic slab it was seeded as
+    ref = qgamd.State(m, P_local=16).initialise()
+    st.run(1, 3)
+    ref.run(1, 3)
+    assert np.array_equal(st.to_numpy("psi"), ref.to_numpy("psi"))
 
 
 def test_slab_checkpoint_needs_its_transport(tmp_path):

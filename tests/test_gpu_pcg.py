@@ -124,18 +124,35 @@ def test_deferred_certificate_fused_in_tendency(env, N, steps):
 
 
 def test_deferred_certificate_failure_is_reported(env):
-    """A target below the roundoff floor: every deferred certificate fails; the run is not
-    blocked, the next qg_synchronize reports QG_ERR_NOT_CONVERGED once, and the certificate
-    record counts the failures from the first solve on."""
+    """A target below the roundoff floor: every deferred certificate fails.  Single steps are
+    not blocked; the next qg_synchronize reports QG_ERR_NOT_CONVERGED once, and the
+    certificate record counts the failures from the first solve on.  qg_run reports it itself
+    at its end (it settles and reads the latch), and a long run stops within two polling
+    intervals (QG_PACE_STEPS = 16 steps) of the first failure instead of stepping on."""
     torch, qg, R, O = env
     st = qg.initialise_model(qg.bench_model(64), solver=1, pcg_rtol=1e-30)
-    st.run(1, 5)
+    for t in range(1, 6):
+        st.step(t)
     with pytest.raises(qg.QGError) as e:
         st.synchronize()
     assert e.value.status == -7
     st.synchronize()  # already reported
     c = st.pcg_certificate()
     assert c["solves"] == 5 and c["failures"] == 5 and c["first_failure"] == 1, c
+    # qg_run: reported by the run that hit it, once
+    st2 = qg.initialise_model(qg.bench_model(64), solver=1, pcg_rtol=1e-30)
+    with pytest.raises(qg.QGError) as e:
+        st2.run(1, 5)
+    assert e.value.status == -7
+    st2.synchronize()
+    assert st2.pcg_certificate()["failures"] == 5
+    # a long run stops early (the non-blocking latch poll every 16 steps)
+    st3 = qg.initialise_model(qg.bench_model(64), solver=1, pcg_rtol=1e-30)
+    with pytest.raises(qg.QGError) as e:
+        st3.run(1, 400)
+    assert e.value.status == -7
+    c3 = st3.pcg_certificate()
+    assert 16 <= c3["solves"] <= 3 * 16 + 1 and c3["failures"] == c3["solves"], c3
 
 
 def test_deferred_pcg_graph_replay(env, monkeypatch):
