@@ -128,7 +128,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     double *hline = a.hline;
     // register prefetch: row j-1 is loaded while row j is transformed (the barriers only wait
     // for LDS traffic, so the global loads stay in flight across the FFT)
-    double pf1[EP], pf2[EP];
+    // (the storage type until used: F32 values converted at the load would make it wait at once)
+    S pf1[EP], pf2[EP];
     auto load_into = [&](int j, auto &d1, auto &d2) {
         const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
         const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
 #else
     constexpr int DEPTH = 1;
 #endif
-    double qf1[EP], qf2[EP];
+    S qf1[EP], qf2[EP];
 #if !defined(QG_PA_COEF_ROW) && !defined(QG_PA_COEF_LATE) && !defined(QG_PA_PF2)
     // r of this thread's lines, loaded once: row-invariant, and at this kernel's register
     // budget (224 VGPRs before at 4096) the values fit without spilling, so no row reloads
@@ -786,7 +787,9 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 
     // register prefetch of the next row of u (in flight across this row's FFT).  Slot (0, t=0)
     // packs the real lines k = 0 (.x) and k = N/2 (.y).
-    double2 upf[KQ][2];
+    // (kept in the storage precision until used: converting F32 values right after the load
+    // would make the load wait at once, so the prefetch would not be in flight at all)
+    US upf[KQ][2];
     auto load_u = [&](int j) {
         const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS;
 #pragma unroll
@@ -794,8 +797,14 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             const int k = t + q * T;
             if (NH % T == 0 || k < NH) {
 #pragma unroll
-                for (int s = 0; s < 2; ++s)
-                    upf[q][s] = k == 0 ? make_double2(Urow[s * KS].x, Urow[s * KS + NH].x) : d2(Urow[s * KS + k]);
+                for (int s = 0; s < 2; ++s) {
+                    if (k == 0) {
+                        upf[q][s].x = Urow[s * KS].x;
+                        upf[q][s].y = Urow[s * KS + NH].x;
+                    } else {
+                        upf[q][s] = Urow[s * KS + k];
+                    }
+                }
             }
         }
     };
@@ -858,7 +867,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 #pragma unroll
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) ucur[q][s] = upf[q][s];
+            for (int s = 0; s < 2; ++s) ucur[q][s] = d2(upf[q][s]);
         if (PF && j < e) load_u(j + 1);
         // compiler memory barrier: re-read the (L1-resident) coefficients every row instead of
         // hoisting them into registers, which would spill at this occupancy
@@ -1023,35 +1032,53 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     }
     double dc = 0;
     PV pf1[HK], pf2[HK];
-    auto load_row = [&](int j) {
+    auto load_row = [&](int j, PV(&d1)[HK], PV(&d2)[HK]) {
         const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
         const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
 #pragma unroll
         for (int p = 0; p < HK; ++p) {
             const int n = t + p * HT;
-            pf1[p] = *reinterpret_cast<const PV *>(r1 + 2 * n);
-            pf2[p] = *reinterpret_cast<const PV *>(r2 + 2 * n);
+            d1[p] = *reinterpret_cast<const PV *>(r1 + 2 * n);
+            d2[p] = *reinterpret_cast<const PV *>(r2 + 2 * n);
         }
     };
-    load_row(e);
     const double *cr = a.cr + s * KS;
     const double csc = a.csc;
-    for (int j = e; j >= s0; --j) {
+    // one row: consume the prefetched row (c1, c2), refill them with row jn (< s0: none)
+    auto row_step = [&](int j, PV(&c1)[HK], PV(&c2)[HK], int jn) {
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop
+#if defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)
+        // two rows in flight: this row's r must be issued before the refill (loads complete
+        // in order, so a later r load would wait for both prefetched rows)
+        double rq[HK], rNq = 0;
+#pragma unroll
+        for (int q = 0; q < HK; ++q) rq[q] = cr[t + q * HT];
+        if (t == 0) rNq = cr[HN];
+#endif
         double2 in[HK];
 #pragma unroll
         for (int p = 0; p < HK; ++p)
-            in[p] = make_double2(pa * (double)pf1[p].x + pb * (double)pf2[p].x,
-                                 pa * (double)pf1[p].y + pb * (double)pf2[p].y);
+            in[p] = make_double2(pa * (double)c1[p].x + pb * (double)c2[p].x,
+                                 pa * (double)c1[p].y + pb * (double)c2[p].y);
         // first pass from registers, then the next row's loads (in[] is dead by then: fewer
         // live registers than loading first), then the remaining passes
         const int tt = opaque_tid();
+#ifdef QG_EXP_NOFFT  // timing experiment only (wrong results): the row, untransformed
+        {
+            double2 *Zw = const_cast<double2 *>(Zb);
+#pragma unroll
+            for (int p = 0; p < HK; ++p) Zw[lay<HPlan::LAST_NS>(t + p * HT)] = in[p];
+            if (jn >= s0) load_row(jn, c1, c2);
+            __syncthreads();
+        }
+#else
         fft_pass<HN, HT, 1, 0, false, true, false>(nullptr, b0, twl, tt, in);
-        if (j > s0) load_row(j - 1);
+        if (jn >= s0) load_row(jn, c1, c2);
         {
             double2 dummy[HPlan::R_LAST];
             fft_run<HN, HT, HPlan::R0, 1, false, false>(b0, b1, twl, tt, dummy);
         }
+#endif
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
@@ -1063,7 +1090,11 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                     dc += X0;
                     a.hline[j] = X0;
                 }
+#if defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)
+                const double r0 = rq[q], rN = rNq;
+#else
                 const double r0 = cr[0], rN = cr[HN];
+#endif
                 u[q] = make_double2((r0 * csc) * X0 + r0 * u[q].x, (rN * csc) * XN + rN * u[q].y);
                 Urow[0] = Store<S>::c(make_double2(u[q].x, 0));
                 Urow[HN] = Store<S>::c(make_double2(u[q].y, 0));
@@ -1075,7 +1106,11 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                 const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
                 const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
+#if defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)
+                const double r = rq[q];
+#else
                 const double r = cr[k];
+#endif
                 u[q] = cfma(r, u[q], cscale(X, r * csc));
                 Urow[k] = Store<S>::c(u[q]);
                 bw[q] = cfma(om[q].x, u[q], bw[q]);
@@ -1083,7 +1118,19 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
             }
         }
         if constexpr (Fwd::b0_read_late) __syncthreads();  // the next row's first pass writes b0
+    };
+#ifdef QG_PAH_PF2
+    PV qf1[HK], qf2[HK];
+    load_row(e, pf1, pf2);
+    if (e - 1 >= s0) load_row(e - 1, qf1, qf2);
+    for (int j = e; j >= s0; j -= 2) {
+        row_step(j, pf1, pf2, j - 2);
+        if (j - 1 >= s0) row_step(j - 1, qf1, qf2, j - 3);
     }
+#else
+    load_row(e, pf1, pf2);
+    for (int j = e; j >= s0; --j) row_step(j, pf1, pf2, j - 1);
+#endif
 #pragma unroll
     for (int q = 0; q < HK; ++q) {
         const int k = t + q * HT;
@@ -1134,13 +1181,18 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     const double2 *crr = a.crr + s * KS;
     const double *ccs = a.ccs + s * KS;
 
-    double2 upf[HK];
+    US upf[HK];  // (storage precision until used: see spec_passB)
     auto load_u = [&](int j) {
         const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
             const int k = t + q * HT;
-            upf[q] = k == 0 ? make_double2(Urow[0].x, Urow[HN].x) : d2(Urow[k]);
+            if (k == 0) {
+                upf[q].x = Urow[0].x;
+                upf[q].y = Urow[HN].x;
+            } else {
+                upf[q] = Urow[k];
+            }
         }
     };
     load_u(s0);
@@ -1183,7 +1235,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     for (int j = s0; j <= e; ++j) {
         double2 ucur[HK];
 #pragma unroll
-        for (int q = 0; q < HK; ++q) ucur[q] = upf[q];
+        for (int q = 0; q < HK; ++q) ucur[q] = d2(upf[q]);
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop
         double x0 = 0;  // slot (q 0, t 0): X_0 (.x of w, or the singular line)
 #pragma unroll
@@ -1228,6 +1280,17 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
         }
         // first inverse pass, then the next row's loads (in[] dead), then the remaining passes
         const int tt = opaque_tid();
+#ifdef QG_EXP_NOFFT  // timing experiment only (wrong results)
+        {
+            double2 *Xw = const_cast<double2 *>(Xb);
+            __syncthreads();  // (Xs = b1 may be Xb: every partner read above is done)
+#pragma unroll
+            for (int q = 0; q < HK; ++q) Xw[lay<HPlan::LAST_NS>(t + q * HT)] = in[q];
+            if (j < e) load_u(j + 1);
+            if constexpr (SYS == 1) load_y(j);
+            __syncthreads();
+        }
+#else
         fft_pass<HN, HT, 1, 0, true, true, false>(nullptr, b0, twl, tt, in);
         if (j < e) load_u(j + 1);
         if constexpr (SYS == 1) load_y(j);
@@ -1235,6 +1298,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
             double2 dummy[HPlan::R_LAST];
             fft_run<HN, HT, HPlan::R0, 1, true, false>(b0, b1, twl, tt, dummy);
         }
+#endif
         if constexpr (SYS == 0) {
             S *yr = static_cast<S *>(a.half_tmp) + (size_t)j * a.M;
             const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;

@@ -446,8 +446,13 @@ __device__ __forceinline__ void store_pair_with_ghosts(T *row, T *grow, int M, i
     if (grow) put(grow);
 }
 
+#ifdef QG_PAIR_MINW  // experiment: waves per SIMD the registers must allow
+template <int TX, class T>
+__global__ __launch_bounds__(TX, QG_PAIR_MINW) void tendency_pair_kernel(TendArgsT<T> a, int nyA, int nyB) {
+#else
 template <int TX, class T>
 __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int nyA, int nyB) {
+#endif
     using V = typename PairT<T>::V;
     using VU = typename PairT<T>::VU;
     constexpr int RP = 6, RZ = 5, RL = 4, W = 2 * TX, WL = W + 4;
@@ -714,33 +719,25 @@ struct SlotMoveArgs {
     int64_t n16;
 };
 
-constexpr int SLOT_MOVE_V = 4;  // vectors per thread and slot: all loads in flight before the stores
+// One vector per thread and slot, non-temporal stores (tools/microbench/slot_shift.hip, two
+// 4096^2 F64 arrays shifted: 5.7 TB/s of reads + writes; 4 vectors per thread with all loads
+// first 4.5, grid-stride loops 4.7-5.2, plain stores 5.5, hipMemcpyAsync pairs 5.4)
+typedef unsigned int SlotVec __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(256) void slot_move_kernel(SlotMoveArgs a) {
     const int k = blockIdx.y;
-    uint4 *b = a.base[k];
+    SlotVec *b = reinterpret_cast<SlotVec *>(a.base[k]);
     const int s0 = a.src[k][0], s1 = a.src[k][1], s2 = a.src[k][2];
     const int64_t n = a.n16;
-    const int64_t i0 = (int64_t)blockIdx.x * (256 * SLOT_MOVE_V) + threadIdx.x;
-    uint4 v[3][SLOT_MOVE_V];
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    SlotVec v[3];
 #pragma unroll
     for (int q = 0; q < 3; ++q)
-        if (s0 == q || s1 == q || s2 == q) {
-#pragma unroll
-            for (int u = 0; u < SLOT_MOVE_V; ++u) {
-                const int64_t i = i0 + u * 256;
-                if (i < n) v[q][u] = b[q * n + i];
-            }
-        }
-#pragma unroll
-    for (int u = 0; u < SLOT_MOVE_V; ++u) {
-        const int64_t i = i0 + u * 256;
-        if (i < n) {
-            if (s0 >= 0) b[i] = v[s0][u];
-            if (s1 >= 0) b[n + i] = v[s1][u];
-            if (s2 >= 0) b[2 * n + i] = v[s2][u];
-        }
-    }
+        if (s0 == q || s1 == q || s2 == q) v[q] = b[q * n + i];
+    if (s0 >= 0) __builtin_nontemporal_store(v[s0], b + i);
+    if (s1 >= 0) __builtin_nontemporal_store(v[s1], b + n + i);
+    if (s2 >= 0) __builtin_nontemporal_store(v[s2], b + 2 * n + i);
 }
 
 int launch_slot_move(void *const *arrays, const int (*src)[3], int narrays, size_t slot_bytes, hipStream_t s) {
@@ -755,7 +752,7 @@ int launch_slot_move(void *const *arrays, const int (*src)[3], int narrays, size
         }
     }
     a.n16 = (int64_t)(slot_bytes / 16);
-    const int64_t gx = (a.n16 + 256 * SLOT_MOVE_V - 1) / (256 * SLOT_MOVE_V);
+    const int64_t gx = (a.n16 + 255) / 256;
     if (gx > 0x7fffffff) return QG_ERR_UNSUPPORTED;
     slot_move_kernel<<<dim3((unsigned)std::max<int64_t>(gx, 1), (unsigned)narrays), 256, 0, s>>>(a);
     QG_LAUNCH_CHECK();
