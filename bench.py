@@ -230,7 +230,8 @@ def validate_record(out):
         for key, spec in (("comm", _COMM), ("overlap_ab", _OVERLAP_AB)):
             if key not in out:
                 raise ValueError(f"multi-GPU record: missing {key}")
-            need(out[key], spec, key)
+            if "error" not in out[key]:  # (a failed leg is reported, not silently dropped)
+                need(out[key], spec, key)
     return True
 
 
@@ -374,37 +375,62 @@ def main():
     # multi-GPU: the two collectives of a step timed in isolation, then the same K steps with
     # the halo / interior overlap toggled (all ranks take part in both)
     comm, overlap_ab = None, None
+    dev_red = "cuda" if args.transport == "rccl" else "cpu"
+
+    def all_ok(ok):
+        # every rank learns whether every rank's leg succeeded (over torch's own process
+        # group), so a failed leg is skipped by all ranks together and the headline line
+        # below is still printed
+        if dist is None:
+            return ok
+        f = torch.tensor([1 if ok else 0], dtype=torch.int64, device=dev_red)
+        dist.all_reduce(f, op=dist.ReduceOp.MIN)
+        return bool(f.item())
+
     if args.comm_probe_reps > 0 and (world > 1 or args.comm_self) and args.solver == "spectral":
-        comm = st.comm_probe(args.comm_probe_reps)
-        if dist is not None:
-            cv = torch.tensor([comm["halo_ms"], comm["allgather_ms"]], dtype=torch.float64,
-                              device="cuda" if args.transport == "rccl" else "cpu")
-            dist.all_reduce(cv, op=dist.ReduceOp.MAX)
-            comm["halo_ms_max_over_ranks"], comm["allgather_ms_max_over_ranks"] = float(cv[0]), float(cv[1])
-        comm["share_of_step"] = (comm.get("halo_ms_max_over_ranks", comm["halo_ms"])
-                                 + comm.get("allgather_ms_max_over_ranks", comm["allgather_ms"])) / (el * 1e3 / K)
-        st.set_overlap(not args.overlap)
-        for _ in range(3):
-            st.step(t)
-            t += 1
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        st.run(t, K)
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        el2 = time.perf_counter() - t1
-        t += K
-        if dist is not None:
-            tt = torch.tensor([el2], dtype=torch.float64, device="cuda" if args.transport == "rccl" else "cpu")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el2 = float(tt.item())
-        st.set_overlap(args.overlap)
-        overlap_ab = {"halo_overlap": not args.overlap, "value": world * K / el2, "ms_per_step": el2 * 1e3 / K,
-                      "steps": K, "note": "the same K steps re-timed in this invocation with qg_set_overlap "
-                                          "toggled (the headline value uses halo_overlap of config)"}
+        err = None
+        try:
+            comm = st.comm_probe(args.comm_probe_reps)
+        except Exception as e:  # noqa: BLE001 -- reported in the record
+            err = f"{type(e).__name__}: {e}"
+        if all_ok(err is None):
+            if dist is not None:
+                cv = torch.tensor([comm["halo_ms"], comm["allgather_ms"]], dtype=torch.float64, device=dev_red)
+                dist.all_reduce(cv, op=dist.ReduceOp.MAX)
+                comm["halo_ms_max_over_ranks"], comm["allgather_ms_max_over_ranks"] = float(cv[0]), float(cv[1])
+            comm["share_of_step"] = (comm.get("halo_ms_max_over_ranks", comm["halo_ms"])
+                                     + comm.get("allgather_ms_max_over_ranks", comm["allgather_ms"])) / (el * 1e3 / K)
+            err2, el2 = None, None
+            try:
+                st.set_overlap(not args.overlap)
+                for _ in range(3):
+                    st.step(t)
+                    t += 1
+                if dist is not None:
+                    dist.barrier()
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                st.run(t, K)
+                torch.cuda.synchronize()
+                el2 = time.perf_counter() - t1
+                t += K
+                st.set_overlap(args.overlap)
+            except Exception as e:  # noqa: BLE001
+                err2 = f"{type(e).__name__}: {e}"
+            if all_ok(err2 is None):
+                if dist is not None:
+                    tt = torch.tensor([el2], dtype=torch.float64, device=dev_red)
+                    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                    el2 = float(tt.item())
+                overlap_ab = {"halo_overlap": not args.overlap, "value": world * K / el2,
+                              "ms_per_step": el2 * 1e3 / K, "steps": K,
+                              "note": "the same K steps re-timed in this invocation with qg_set_overlap "
+                                      "toggled (the headline value uses halo_overlap of config)"}
+            else:
+                overlap_ab = {"error": err2 or "failed on another rank"}
+        else:
+            comm = {"error": err or "failed on another rank"}
+            overlap_ab = {"error": "skipped: the comm probe failed"}
 
     if rank != 0:
         if dist is not None:
@@ -485,8 +511,11 @@ def main():
             and not args.comm_self:
         del st
         torch.cuda.empty_cache()
-        d = dropin_variant(qgamd, m, n, 3, args.dropin_steps, torch)
-        d["vs_qg_run_step"] = d["ms_per_step"] / ms
+        try:
+            d = dropin_variant(qgamd, m, n, 3, args.dropin_steps, torch)
+            d["vs_qg_run_step"] = d["ms_per_step"] / ms
+        except Exception as e:  # noqa: BLE001 -- reported, the headline line is still printed
+            d = {"error": f"{type(e).__name__}: {e}"}
         out["dropin"] = d
     if args.cpu_steps > 0 and world == 1 and args.dtype == "f64":
         out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads, args.cpu_steps_1t)

@@ -446,13 +446,9 @@ __device__ __forceinline__ void store_pair_with_ghosts(T *row, T *grow, int M, i
     if (grow) put(grow);
 }
 
-#ifdef QG_PAIR_MINW  // experiment: waves per SIMD the registers must allow
-template <int TX, class T>
-__global__ __launch_bounds__(TX, QG_PAIR_MINW) void tendency_pair_kernel(TendArgsT<T> a, int nyA, int nyB) {
-#else
-template <int TX, class T>
+// PF: register prefetch depth in rows (as tendency_kernel's)
+template <int TX, class T, int PF = 1>
 __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int nyA, int nyB) {
-#endif
     using V = typename PairT<T>::V;
     using VU = typename PairT<T>::VU;
     constexpr int RP = 6, RZ = 5, RL = 4, W = 2 * TX, WL = W + 4;
@@ -510,7 +506,10 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
     auto load_halo = [&](const T *r, V &h) {
         if (hq >= 0) h = V{r[wx(xh)], r[wx(xh + 1)]};
     };
-    V pc = {0, 0}, ph = {0, 0}, zc = {0, 0}, zh = {0, 0}, f1 = {0, 0}, f2 = {0, 0};
+    // prefetch pipeline PF rows deep: slot 0 is consumed next
+    V pc[PF], ph[PF], zc[PF], zh[PF], f1[PF], f2[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) pc[k] = ph[k] = zc[k] = zh[k] = f1[k] = f2[k] = V{0, 0};
     auto fetch_psi = [&](int j, V &c, V &h) {
         const T *r = rowp(psi, prs, j);
         load_pair(r, c);
@@ -587,11 +586,15 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
         for (int k = 0; k < 3; ++k) commit(sz[ring(jb0 - 1 + k, RZ)], z0c[k], z0h[k]);
     }
 #endif
-    if (jb0 + 2 <= jb1) {
-        fetch_psi(jb0 + 3, pc, ph);
-        fetch_zeta(jb0 + 2, zc, zh);
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+        const int j = jb0 + k;
+        if (j + 2 <= jb1) {
+            fetch_psi(j + 3, pc[k], ph[k]);
+            fetch_zeta(j + 2, zc[k], zh[k]);
+        }
+        if (j < jb1) fetch_f(j, f1[k], f2[k]);
     }
-    fetch_f(jb0, f1, f2);
     __syncthreads();
     lap_row(jb0 - 1);
     lap_row(jb0);
@@ -603,18 +606,30 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
     for (int j = jb0; j < jb1; ++j) {
         const bool more = j + 2 <= jb1;
         if (more) {
-            commit(sp[ring(j + 3, RP)], pc, ph);
-            commit(sz[ring(j + 2, RZ)], zc, zh);
+            commit(sp[ring(j + 3, RP)], pc[0], ph[0]);
+            commit(sz[ring(j + 2, RZ)], zc[0], zh[0]);
         }
-        const V f1c = f1, f2c = f2;
+        const V f1c = f1[0], f2c = f2[0];
 #ifndef QG_TEND_LATE_F
         asm volatile("" : : "v"(f1c), "v"(f2c) : "memory");  // (see tendency_kernel)
 #endif
-        if (j + 1 + 2 <= jb1) {
-            fetch_psi(j + 4, pc, ph);
-            fetch_zeta(j + 3, zc, zh);
+#pragma unroll
+        for (int k = 0; k + 1 < PF; ++k) {
+            pc[k] = pc[k + 1];
+            ph[k] = ph[k + 1];
+            zc[k] = zc[k + 1];
+            zh[k] = zh[k + 1];
+            f1[k] = f1[k + 1];
+            f2[k] = f2[k + 1];
         }
-        if (j + 1 < jb1) fetch_f(j + 1, f1, f2);
+        {
+            const int jn = j + PF;  // iteration whose inputs are fetched now
+            if (jn + 2 <= jb1) {
+                fetch_psi(jn + 3, pc[PF - 1], ph[PF - 1]);
+                fetch_zeta(jn + 2, zc[PF - 1], zh[PF - 1]);
+            }
+            if (jn < jb1) fetch_f(jn, f1[PF - 1], f2[PF - 1]);
+        }
         __syncthreads();
         if (more) lap_row(j + 2);
         if (has_a) {
@@ -978,15 +993,18 @@ int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
 
 // Float32 default: the pair kernel over whole chip-fulls of 512-point strips (as above);
 // QG_TEND_PAIR=0 selects the one-point kernel instead.
+#ifndef QG_PAIR_PF
+#define QG_PAIR_PF 1
+#endif
 template <int TX, class T>
 static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
-    constexpr int W = 2 * TX;
+    constexpr int W = 2 * TX, PF = QG_PAIR_PF;
     static int sl = 0;
     if (sl == 0) {
         int dev = 0, cus = 0, per = 0;
         QG_HIP(hipGetDevice(&dev));
         QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_pair_kernel<TX, T>, TX, 0));
+        QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_pair_kernel<TX, T, PF>, TX, 0));
         sl = cus * (per > 0 ? per : 1);
     }
     const char *e = std::getenv("QG_TEND_WAVES");
@@ -1001,7 +1019,7 @@ static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
     dim3 grid((unsigned)nx, (unsigned)(nyA + nyB), 2);
-    tendency_pair_kernel<TX, T><<<grid, TX, 0, s>>>(a, nyA, nyB);
+    tendency_pair_kernel<TX, T, PF><<<grid, TX, 0, s>>>(a, nyA, nyB);
     QG_LAUNCH_CHECK();
     return QG_OK;
 }

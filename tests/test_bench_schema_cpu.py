@@ -58,3 +58,13 @@ def test_single_gpu_record_without_comm_is_valid():
     r["metric"] = "something else"
     with pytest.raises(ValueError):
         bench.validate_record(r)
+
+
+def test_failed_leg_is_reported_not_dropped():
+    """A multi-GPU leg that failed (e.g. an RCCL error in the probe) is recorded as an error
+    sub-record on every rank, and the headline record stays valid."""
+    r = json.loads(open([p for p in _committed() if "rehearsal" in p][0]).read().strip().splitlines()[-1])
+    r = copy.deepcopy(r)
+    r["comm"] = {"error": "QGError: qg_comm_probe failed (-6)"}
+    r["overlap_ab"] = {"error": "skipped: the comm probe failed"}
+    assert bench.validate_record(r)
