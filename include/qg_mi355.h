@@ -157,8 +157,10 @@ int qg_get_stats(qg_ctx *ctx, qg_stats *out);
  * the residual check runs on the device (on one rank fused into the next step's tendency,
  * which reads exactly that solve's zeta and psi; else as its own pass after the solve) and
  * its verdict is latched there: no host round trip, qg_run can replay PCG steps as HIP graphs.
- * A failed certification is reported by the next qg_synchronize (QG_ERR_NOT_CONVERGED) and
- * by qg_pcg_certificate.  sync = 1 (or QG_PCG_SYNC=1 at create): the host reads every
+ * A failed certification is reported (QG_ERR_NOT_CONVERGED, once) by qg_evolve_psi / qg_step
+ * within two polling intervals (the latch is copied to the host every QG_PACE_STEPS solves and
+ * read one interval later, without blocking), by the end of qg_run (it settles and reads the
+ * latch), by qg_synchronize, and in qg_pcg_certificate's record.  sync = 1 (or QG_PCG_SYNC=1 at create): the host reads every
  * residual and runs the general PCG iteration when the certificate fails (the old form).  */
 int qg_set_pcg_sync(qg_ctx *ctx, int sync);
 /* deferred certificates so far: solves certified, failures, first failing solve (1-based,

@@ -477,48 +477,6 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     return c->esize == sizeof(float) ? evolve_zeta_t<float>(c, timestep) : evolve_zeta_t<double>(c, timestep);
 }
 
-int qg_evolve_psi(qg_ctx *c) {
-    if (!c) return QG_ERR_INVALID_ARG;
-    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
-    if (!c->spec && !c->pcg) return QG_ERR_UNSUPPORTED;
-    QG_HIP(hipSetDevice(c->device));
-    const int zh = c->heads[0];
-    int pn = (c->heads[1] + 2) % 3;
-    if (c->keep_order) {  // store_new_state!'s shift of psi, then the solve writes slot 1
-        void *arr[1] = {c->psi};
-        QG_CHECK(launch_slot_shift(arr, 1, 2 * c->esize * c->F, c->stream));
-        pn = 0;
-    }
-    double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);  // (element type p.dtype)
-    const double *z1 = c->field(c->zeta, 0, zh), *z2 = c->field(c->zeta, 1, zh);
-    if (c->pcg) {
-        const int st = c->pcg->solve(z1, z2, o1, o2, !c->distributed, c->stream,
-                                     c->distributed ? comm_allgather : nullptr, c->comm,
-                                     c->distributed ? comm_halo : nullptr, c->comm);
-        c->last_status = st;
-        if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
-    } else {
-        QG_CHECK(c->spec->solve(z1, z2, o1, o2, !c->distributed, c->stream,
-                                c->distributed ? comm_allgather : nullptr, c->comm));
-    }
-    c->heads[1] = pn;
-    if (c->distributed) c->ghosts_pending = true;  // psi's ghost rows: at the next ghost flush
-    return c->pcg ? c->last_status : QG_OK;
-}
-
-// Multi-GPU pacing: every QG_PACE_STEPS steps, wait (bounded) for the event recorded
-// QG_PACE_STEPS steps earlier, then record a new one.  The host stays 1-2 intervals ahead of
-// the device (enough to keep the queue full), and a dead peer surfaces as QG_ERR_RCCL from
-// the watchdog instead of a host blocked inside a launch on a full queue.
-static int pace(qg_ctx *c) {
-    if (!c->distributed || ++c->pace_count % QG_PACE_STEPS != 0) return QG_OK;
-    if (!c->pace_ev) QG_HIP(hipEventCreateWithFlags(&c->pace_ev, hipEventDisableTiming));
-    if (c->pace_armed) QG_CHECK(comm_wait(c->comm, c->stream, c->pace_ev, "qg_run (pacing wait)"));
-    QG_HIP(hipEventRecord(c->pace_ev, c->stream));
-    c->pace_armed = true;
-    return QG_OK;
-}
-
 // Deferred PCG: report new certification failures the device has latched.  Non-blocking
 // (wait = false): every QG_PACE_STEPS steps, read the copy of the latch made one interval
 // earlier if it has landed, then start a new copy.  Blocking (wait = true, the end of qg_run):
@@ -561,12 +519,54 @@ static int poll_pcg(qg_ctx *c, bool wait) {
     return QG_OK;
 }
 
+int qg_evolve_psi(qg_ctx *c) {
+    if (!c) return QG_ERR_INVALID_ARG;
+    if (!c->initialised || !c->zeta) return QG_ERR_NOT_BOUND;
+    if (!c->spec && !c->pcg) return QG_ERR_UNSUPPORTED;
+    QG_HIP(hipSetDevice(c->device));
+    const int zh = c->heads[0];
+    int pn = (c->heads[1] + 2) % 3;
+    if (c->keep_order) {  // store_new_state!'s shift of psi, then the solve writes slot 1
+        void *arr[1] = {c->psi};
+        QG_CHECK(launch_slot_shift(arr, 1, 2 * c->esize * c->F, c->stream));
+        pn = 0;
+    }
+    double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);  // (element type p.dtype)
+    const double *z1 = c->field(c->zeta, 0, zh), *z2 = c->field(c->zeta, 1, zh);
+    if (c->pcg) {
+        const int st = c->pcg->solve(z1, z2, o1, o2, !c->distributed, c->stream,
+                                     c->distributed ? comm_allgather : nullptr, c->comm,
+                                     c->distributed ? comm_halo : nullptr, c->comm);
+        c->last_status = st;
+        if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
+    } else {
+        QG_CHECK(c->spec->solve(z1, z2, o1, o2, !c->distributed, c->stream,
+                                c->distributed ? comm_allgather : nullptr, c->comm));
+    }
+    c->heads[1] = pn;
+    if (c->distributed) c->ghosts_pending = true;  // psi's ghost rows: at the next ghost flush
+    if (c->pcg) QG_CHECK(poll_pcg(c, false));  // deferred certificates: the bounded-delay report
+    return c->pcg ? c->last_status : QG_OK;
+}
+
+// Multi-GPU pacing: every QG_PACE_STEPS steps, wait (bounded) for the event recorded
+// QG_PACE_STEPS steps earlier, then record a new one.  The host stays 1-2 intervals ahead of
+// the device (enough to keep the queue full), and a dead peer surfaces as QG_ERR_RCCL from
+// the watchdog instead of a host blocked inside a launch on a full queue.
+static int pace(qg_ctx *c) {
+    if (!c->distributed || ++c->pace_count % QG_PACE_STEPS != 0) return QG_OK;
+    if (!c->pace_ev) QG_HIP(hipEventCreateWithFlags(&c->pace_ev, hipEventDisableTiming));
+    if (c->pace_armed) QG_CHECK(comm_wait(c->comm, c->stream, c->pace_ev, "qg_run (pacing wait)"));
+    QG_HIP(hipEventRecord(c->pace_ev, c->stream));
+    c->pace_armed = true;
+    return QG_OK;
+}
+
 int qg_step(qg_ctx *c, int64_t timestep) {
     QG_CHECK(qg_evolve_zeta(c, timestep));
     const int st = qg_evolve_psi(c);
     if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
     QG_CHECK(pace(c));
-    QG_CHECK(poll_pcg(c, false));
     return st;
 }
 

@@ -153,6 +153,18 @@ def test_deferred_certificate_failure_is_reported(env):
     assert e.value.status == -7
     c3 = st3.pcg_certificate()
     assert 16 <= c3["solves"] <= 3 * 16 + 1 and c3["failures"] == c3["solves"], c3
+    # the reference's own loop (evolve_zeta! / evolve_psi! per step): evolve_psi! polls too
+    st4 = qg.initialise_model(qg.bench_model(64), solver=1, pcg_rtol=1e-30)
+    stopped = None
+    for t in range(1, 200):
+        st4.evolve_zeta_(t)
+        try:
+            st4.evolve_psi_()
+        except qg.QGError as e:
+            assert e.status == -7
+            stopped = t
+            break
+    assert stopped is not None and 16 <= stopped <= 3 * 16 + 1, stopped
 
 
 def test_deferred_pcg_graph_replay(env, monkeypatch):
