@@ -27,7 +27,7 @@ def _flat(d):
     return np.array([x for k in sorted(d) for x in np.atleast_1d(d[k])])
 
 
-def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0, wind=None, overlap=False):
+def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0, wind=None, overlap=False, keep=False):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
@@ -46,6 +46,8 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0, wind=
     TorchDistTransport().attach(st, world, rank)
     st.set_overlap(overlap)
     st.initialise()
+    if keep:
+        st.set_keep_order(True)
     if resume_at:
         # checkpoint after resume_at steps, rebuild the slab from the file, continue
         st.run(1, resume_at)
@@ -57,6 +59,8 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0, wind=
         st.run(t, steps - resume_at)
     else:
         st.run(1, steps)
+    if keep:
+        assert st.heads() == [0, 0, 0]
     torch.cuda.synchronize()
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), diag=_flat(st.diagnostics()),
              **{n: st.to_numpy(n) for n in ("zeta", "psi", "f_store")})
@@ -112,12 +116,12 @@ def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at, wind):
                 assert err < (1e-10 if M >= 4096 else 1e-12), (r, n, err)
 
 
-def _run_slabs(world, M, P, steps, d, solver=0, overlap=False):
+def _run_slabs(world, M, P, steps, d, solver=0, overlap=False, keep=False):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, 0, None, overlap))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, 0, None, overlap, keep))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -142,3 +146,20 @@ def test_overlap_is_bit_identical(world, M, P, steps, solver):
     for r in range(world):
         for n in ("zeta", "psi", "f_store", "diag"):
             assert np.array_equal(base[r][n], over[r][n]), (r, n)
+
+
+@pytest.mark.parametrize("world,M,P,steps,solver", [(2, 64, 64, 7, 0), (4, 32, 64, 5, 1)])
+def test_keep_order_slabs_bit_identical(world, M, P, steps, solver):
+    """qg_set_keep_order on every slab (the reference's slot order kept on the device: the
+    history shifted in place, ghost rows refreshed lazily with the rest): every slot of every
+    slab bit for bit equal to the rotating default, and the heads stay 0."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with tempfile.TemporaryDirectory() as d0, tempfile.TemporaryDirectory() as d1:
+        base = _run_slabs(world, M, P, steps, d0, solver)
+        keep = _run_slabs(world, M, P, steps, d1, solver, keep=True)
+    for r in range(world):
+        for n in ("zeta", "psi", "f_store", "diag"):
+            assert np.array_equal(base[r][n], keep[r][n]), (r, n)
