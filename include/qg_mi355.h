@@ -65,7 +65,8 @@ typedef enum {
 
 typedef enum {
     QG_SOLVER_SPECTRAL = 0, /* direct: x-DFT + parallel cyclic tridiagonal solve in y;    *
-                             * any M in 3..8192 (M = 2^k: FFT passes), else UNSUPPORTED */
+                             * any M in 3..8192 and even M up to 16384 (M = 2^k: FFT      *
+                             * passes), else UNSUPPORTED                                  */
     QG_SOLVER_PCG = 1       /* matrix-free PCG on the 5-point operator                     */
 } qg_solver_kind;
 

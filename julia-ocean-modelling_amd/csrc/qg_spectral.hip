@@ -1706,6 +1706,7 @@ __global__ __launch_bounds__(GEN_T) void spec_passB_gen(SpecArgs a) {
 // ------------------------------------------------------------------------------------
 constexpr int SPL_T = 512;        // row-transform threads (256 VGPRs: a radix-13 butterfly + its roots)
 constexpr int SPL_MMAX = 8192;    // one LDS buffer of M complex (128 KB)
+constexpr int SPL_WMAX = 2 * SPL_MMAX;  // even rows up to here: one system at a time, half length
 constexpr int SPL_KT = 256;       // recurrence kernels: wavenumbers per workgroup
 
 // One decimation-in-frequency stage of radix R, in place: butterfly (block b, n) reads the R
@@ -1768,15 +1769,17 @@ __device__ void spl_stage(double2 *buf, const double2 *__restrict__ tw, int M, i
 
 // the whole row transform in place (input synchronised in buf, natural order).  Planned rows:
 // result synchronised in buf with frequency k at a.perm[k]; direct DFT: natural order.
+// tw: the M-entry table of exp(-2 pi i m / M) (a.tw for the row length, a.tw2 for the
+// half-length transforms of the wide split rows)
 template <bool INV>
-__device__ void spl_fft(double2 *buf, const SpecArgs &a, int M) {
+__device__ void spl_fft(double2 *buf, const SpecArgs &a, const double2 *tw, int M) {
     if (a.nrad == 0) {  // direct DFT: outputs to registers, then back in place
         constexpr int OUT = SPL_MMAX / SPL_T;
         double2 o[OUT];
 #pragma unroll
         for (int q = 0; q < OUT; ++q) {
             const int k = threadIdx.x + q * SPL_T;
-            if (k < M) o[q] = dft_at<INV>(buf, a.tw, M, k);
+            if (k < M) o[q] = dft_at<INV>(buf, tw, M, k);
         }
         __syncthreads();
 #pragma unroll
@@ -1792,14 +1795,14 @@ __device__ void spl_fft(double2 *buf, const SpecArgs &a, int M) {
         const int R = a.rad[p];
         span /= R;
         switch (R) {
-            case 2: spl_stage<2, INV>(buf, a.tw, M, span); break;
-            case 3: spl_stage<3, INV>(buf, a.tw, M, span); break;
-            case 4: spl_stage<4, INV>(buf, a.tw, M, span); break;
-            case 5: spl_stage<5, INV>(buf, a.tw, M, span); break;
-            case 7: spl_stage<7, INV>(buf, a.tw, M, span); break;
-            case 8: spl_stage<8, INV>(buf, a.tw, M, span); break;
-            case 11: spl_stage<11, INV>(buf, a.tw, M, span); break;
-            default: spl_stage<13, INV>(buf, a.tw, M, span); break;
+            case 2: spl_stage<2, INV>(buf, tw, M, span); break;
+            case 3: spl_stage<3, INV>(buf, tw, M, span); break;
+            case 4: spl_stage<4, INV>(buf, tw, M, span); break;
+            case 5: spl_stage<5, INV>(buf, tw, M, span); break;
+            case 7: spl_stage<7, INV>(buf, tw, M, span); break;
+            case 8: spl_stage<8, INV>(buf, tw, M, span); break;
+            case 11: spl_stage<11, INV>(buf, tw, M, span); break;
+            default: spl_stage<13, INV>(buf, tw, M, span); break;
         }
     }
 }
@@ -1831,7 +1834,7 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
                 buf[i] = make_double2(p0 * z1 + p1 * z2, p2 * z1 + p3 * z2);
             }
             __syncthreads();
-            spl_fft<false>(buf, a, M);
+            spl_fft<false>(buf, a, a.tw, M);
             auto Z = [&](int k) { return buf[a.nrad ? a.perm[k] : k]; };
             for (int k = t; k < KC; k += SPL_T) {
                 const double2 Zk = Z(k);
@@ -1862,7 +1865,7 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
                 }
             }
             __syncthreads();
-            spl_fft<true>(buf, a, M);
+            spl_fft<true>(buf, a, a.tw, M);
             S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
             S *row1 = out1 + (size_t)(j + 1) * ld;
             const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
@@ -1876,6 +1879,118 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
                 if (row2) store_row_with_ghosts(row2, grow2, M, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
             }
             __syncthreads();  // the next row overwrites buf
+        }
+    }
+}
+
+// Even rows wider than SPL_MMAX (up to SPL_WMAX = 16384): the M complex values of a row no
+// longer fit in one LDS buffer, so each system's REAL row x is transformed on its own as the
+// H = M/2-point complex transform of z_n = x_2n + i x_2n+1 (in place in H complex of LDS, the
+// plan and twiddles of length H) plus a split step X_k = E_k + W^k O_k (E, O from Z_k and
+// conj Z_{H-k}), as the wide-row passes do; the inverse rebuilds Z_k = (X_k + conj X_{H-k}) +
+// i W^-k (X_k - conj X_{H-k}).  The inverse keeps system 0's values in registers while system
+// 1 is transformed, then back-projects and stores both.  U, the recurrences, the carries and
+// the closure are the split path's.  A capability path (the reference factors any M x P).
+template <class S, bool INV>
+__global__ __launch_bounds__(SPL_T) void spec_fft_wide(SpecArgs a) {
+    using US = typename Store<S>::C;
+    const int M = (int)a.M, H = M / 2, t = threadIdx.x;
+    const int KS = a.KS;
+    const int64_t Pl = a.P, ld = a.ld;
+    const double2 *twM = a.tw, *twH = a.tw2;
+    extern __shared__ double2 buf[];
+    __shared__ double pinw[SPL_T / 64];
+    constexpr int PER = SPL_MMAX / SPL_T;  // z values per thread (H <= SPL_MMAX)
+    auto Zat = [&](int k) { return buf[a.nrad ? a.perm[k] : k]; };
+    double pin = 0;
+    if constexpr (INV) {
+        const double pinp = a.pinned0 ? pin_part<SPL_T>(a, t) : 0.0;
+        pin = pin_total<SPL_T>(pinp, pinw);
+        if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
+    }
+    for (int64_t j = blockIdx.x; j < Pl; j += gridDim.x) {
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
+        if constexpr (!INV) {
+            const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
+            const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
+            for (int s = 0; s < 2; ++s) {
+                const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];
+                for (int n = t; n < H; n += SPL_T) {
+                    const double xa = pa * (double)r1[2 * n] + pb * (double)r2[2 * n];
+                    const double xb = pa * (double)r1[2 * n + 1] + pb * (double)r2[2 * n + 1];
+                    buf[n] = make_double2(xa, xb);
+                }
+                __syncthreads();
+                spl_fft<false>(buf, a, twH, H);
+                US *Us = Urow + (size_t)s * KS;
+                for (int k = t; k < H; k += SPL_T) {
+                    const double2 Zk = Zat(k);
+                    if (k == 0) {  // X_0 = Re + Im, X_H = Re - Im (both real)
+                        Us[0] = Store<S>::c(make_double2(Zk.x + Zk.y, 0));
+                        Us[H] = Store<S>::c(make_double2(Zk.x - Zk.y, 0));
+                    } else {
+                        const double2 Zm = Zat(H - k);
+                        const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
+                        const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
+                        Us[k] = Store<S>::c(cadd(E, cmul(twM[k], O)));
+                    }
+                }
+                __syncthreads();  // the next transform overwrites buf
+            }
+        } else {
+            double2 z1[PER];  // system 0's z_n (n = t + p SPL_T), pin applied
+            for (int s = 0; s < 2; ++s) {
+                const US *Us = Urow + (size_t)s * KS;
+                for (int k = t; k < H; k += SPL_T) {
+                    if (k == 0) {
+                        const double X0 = d2(Us[0]).x, XH = d2(Us[H]).x;
+                        buf[0] = make_double2(X0 + XH, X0 - XH);
+                    } else {
+                        const double2 Xk = d2(Us[k]), Xm = d2(Us[H - k]);
+                        const double2 A = make_double2(Xk.x + Xm.x, Xk.y - Xm.y);
+                        const double2 D = make_double2(Xk.x - Xm.x, Xk.y + Xm.y);
+                        const double2 B = cmul(cconj(twM[k]), D);
+                        buf[k] = make_double2(A.x - B.y, A.y + B.x);
+                    }
+                }
+                __syncthreads();
+                spl_fft<true>(buf, a, twH, H);
+                if (s == 0) {
+                    const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
+#pragma unroll
+                    for (int p = 0; p < PER; ++p) {
+                        const int n = t + p * SPL_T;
+                        if (n < H) {
+                            const double2 z = Zat(n);
+                            // the pinned unknown is exactly 0 (see spec_passB)
+                            z1[p] = make_double2((pin_row && n == 0) ? 0.0 : z.x - pin, z.y - pin);
+                        }
+                    }
+                    __syncthreads();  // system 1 overwrites buf
+                } else {
+                    S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
+                    S *row1 = out1 + (size_t)(j + 1) * ld;
+                    S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
+                    S *row2 = out2 ? out2 + (size_t)(j + 1) * ld : nullptr;
+                    S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
+#pragma unroll
+                    for (int p = 0; p < PER; ++p) {
+                        const int n = t + p * SPL_T;
+                        if (n < H) {
+                            const double2 z2 = Zat(n);
+                            const double x1a = z1[p].x, x1b = z1[p].y;
+                            store_row_with_ghosts(row1, grow1, M, 2 * n, (S)(a.pin_out[0] * x1a + a.pin_out[1] * z2.x));
+                            store_row_with_ghosts(row1, grow1, M, 2 * n + 1, (S)(a.pin_out[0] * x1b + a.pin_out[1] * z2.y));
+                            if (row2) {
+                                store_row_with_ghosts(row2, grow2, M, 2 * n, (S)(a.pin_out[2] * x1a + a.pin_out[3] * z2.x));
+                                store_row_with_ghosts(row2, grow2, M, 2 * n + 1,
+                                                      (S)(a.pin_out[2] * x1b + a.pin_out[3] * z2.y));
+                            }
+                        }
+                    }
+                    __syncthreads();  // the next row overwrites buf
+                }
+            }
         }
     }
 }
@@ -1992,8 +2107,9 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
     }
     // (QG_SPLIT_FORCE: tests run generic-size rows through the split passes)
     if (a.M > GEN_MMAX || std::getenv("QG_SPLIT_FORCE") != nullptr) {
-        if (a.M > SPL_MMAX) return QG_ERR_UNSUPPORTED;
-        const size_t lds = sizeof(double2) * (size_t)a.M;
+        if (a.M > SPL_WMAX || (a.M > SPL_MMAX && a.M % 2 != 0)) return QG_ERR_UNSUPPORTED;
+        const bool wsplit = a.M > SPL_MMAX;  // half-length transforms, one system at a time
+        const size_t lds = sizeof(double2) * (size_t)(wsplit ? a.M / 2 : a.M);
         const unsigned rows = (unsigned)std::min<int64_t>(a.P, 1024);
         const dim3 rgrid((unsigned)a.Nc, (unsigned)((a.KH + SPL_KT - 1) / SPL_KT));
         auto fft = [&](const void *fn, auto kernel) -> int {
@@ -2003,8 +2119,12 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
             return QG_OK;
         };
         if (!passB) {
-            QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, false>, spec_fft_split<float, false>)
-                           : fft((const void *)spec_fft_split<double, false>, spec_fft_split<double, false>));
+            if (wsplit)
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, false>, spec_fft_wide<float, false>)
+                               : fft((const void *)spec_fft_wide<double, false>, spec_fft_wide<double, false>));
+            else
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, false>, spec_fft_split<float, false>)
+                               : fft((const void *)spec_fft_split<double, false>, spec_fft_split<double, false>));
             if (a.f32) spec_passA_split<float><<<rgrid, SPL_KT, 0, s>>>(a);
             else spec_passA_split<double><<<rgrid, SPL_KT, 0, s>>>(a);
             QG_LAUNCH_CHECK();
@@ -2012,8 +2132,12 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
             if (a.f32) spec_passB_split<float><<<rgrid, SPL_KT, 0, s>>>(a);
             else spec_passB_split<double><<<rgrid, SPL_KT, 0, s>>>(a);
             QG_LAUNCH_CHECK();
-            QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, true>, spec_fft_split<float, true>)
-                           : fft((const void *)spec_fft_split<double, true>, spec_fft_split<double, true>));
+            if (wsplit)
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, true>, spec_fft_wide<float, true>)
+                               : fft((const void *)spec_fft_wide<double, true>, spec_fft_wide<double, true>));
+            else
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, true>, spec_fft_split<float, true>)
+                               : fft((const void *)spec_fft_split<double, true>, spec_fft_split<double, true>));
         }
         return QG_OK;
     }
@@ -2039,6 +2163,7 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
 bool SpectralSolver::supports(int64_t M, int64_t P) {
     if (P < 2) return false;
     if (M >= 8 && M <= 8192 && (M & (M - 1)) == 0) return true;
+    if (M > SPL_MMAX) return M <= SPL_WMAX && M % 2 == 0;  // wide split rows
     return M >= 3 && M <= SPL_MMAX;
 }
 
@@ -2079,8 +2204,9 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.nrad = 0;
     // generic rows: mixed-radix plan, or none (direct DFT: rows with a prime factor > 13, and
     // short rows, where the direct DFT measured no slower -- 120^2: 15 600-17 200 vs 15 000 steps/s)
-    if ((M & (M - 1)) != 0 && M > 128) {
-        int64_t m = M, n = 0;
+    const bool wsplit = M > SPL_MMAX;  // (planned at the half length H = M/2)
+    if (wsplit || ((M & (M - 1)) != 0 && M > 128)) {
+        int64_t m = wsplit ? M / 2 : M, n = 0;
         int rad[16];
         while (m % 8 == 0) { rad[n++] = 8; m /= 8; }
         if (m % 4 == 0) { rad[n++] = 4; m /= 4; }
@@ -2150,10 +2276,11 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     // zero-padded to PIN_PAD parts: every pass B thread loads one unconditionally (pin_part)
     const size_t n_pinpart = align_up(sizeof(double) * (std::max({pin_kblocks(a.KH), nkb, PIN_PAD}) + 1));
     const bool wide = M == 2 * HN;  // wide-row passes: half-length twiddles + system-0 rows
-    const size_t n_tw2 = wide ? align_up(sizeof(double2) * HN) : 0;
+    const size_t n_tw2 = (wide || wsplit) ? align_up(sizeof(double2) * (size_t)(M / 2)) : 0;
     const size_t n_half = wide ? align_up((f32 ? sizeof(float) : sizeof(double)) * (size_t)P * M) : 0;
     // split passes with a plan: where the DIF stages leave frequency k (digit reversal)
-    const size_t n_perm = a.nrad > 0 ? align_up(sizeof(int) * M) : 0;
+    const int64_t MP = wsplit ? M / 2 : M;  // length of the planned transform
+    const size_t n_perm = a.nrad > 0 ? align_up(sizeof(int) * MP) : 0;
     bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart +
              n_tw2 + n_half + n_perm;
     if (hipMalloc(&mem_, bytes_) != hipSuccess) {
@@ -2180,14 +2307,14 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.hline = (double *)take(n_line);
     a.scal = (double *)take(n_scal);
     a.pinpart = (double *)take(n_pinpart);
-    a.tw2 = wide ? (const double2 *)take(n_tw2) : nullptr;
+    a.tw2 = (wide || wsplit) ? (const double2 *)take(n_tw2) : nullptr;
     a.half_tmp = wide ? (void *)take(n_half) : nullptr;
     a.perm = nullptr;
     if (a.nrad > 0) {
         int *d_perm = (int *)take(n_perm);
-        std::vector<int> perm(M);
-        for (int64_t k = 0; k < M; ++k) {
-            int64_t rem = k, span = M, pos = 0;
+        std::vector<int> perm(MP);
+        for (int64_t k = 0; k < MP; ++k) {
+            int64_t rem = k, span = MP, pos = 0;
             for (int q = 0; q < a.nrad; ++q) {
                 span /= a.rad[q];
                 pos += (rem % a.rad[q]) * span;
@@ -2195,16 +2322,17 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
             }
             perm[k] = (int)pos;
         }
-        QG_HIP(hipMemcpy(d_perm, perm.data(), sizeof(int) * M, hipMemcpyHostToDevice));
+        QG_HIP(hipMemcpy(d_perm, perm.data(), sizeof(int) * MP, hipMemcpyHostToDevice));
         a.perm = d_perm;
     }
     a.tw = d_tw;
     a.coef = d_coef;
     QG_HIP(hipMemcpy(d_tw, tw.data(), sizeof(double2) * M, hipMemcpyHostToDevice));
-    if (wide) {  // exp(-2 pi i m / (M/2)) = tw[2m]
-        std::vector<double2> tw2(HN);
-        for (int m = 0; m < HN; ++m) tw2[m] = tw[2 * m];
-        QG_HIP(hipMemcpy((void *)a.tw2, tw2.data(), sizeof(double2) * HN, hipMemcpyHostToDevice));
+    if (wide || wsplit) {  // exp(-2 pi i m / (M/2)) = tw[2m]
+        const int64_t H = M / 2;
+        std::vector<double2> tw2(H);
+        for (int64_t m = 0; m < H; ++m) tw2[m] = tw[2 * m];
+        QG_HIP(hipMemcpy((void *)a.tw2, tw2.data(), sizeof(double2) * H, hipMemcpyHostToDevice));
     }
     QG_HIP(hipMemcpy(d_coef, coef.data(), sizeof(Coef) * coef.size(), hipMemcpyHostToDevice));
     {

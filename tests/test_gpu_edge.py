@@ -13,6 +13,25 @@ def rel(a, b):
     return float(np.linalg.norm(a - b) / np.linalg.norm(b))
 
 
+def modal_residuals(R, m, zeta, psi):
+    """Relative residuals ||A x - b|| / ||b|| of the two modal systems evolve_psi solves
+    (model.jl:172-199), x recovered from the newest psi slot: the pinned Poisson system
+    (laplacian.jl:66-75) and the modified Helmholtz system (laplacian.jl:60-64).  A
+    solver-independent exactness check where two exact solvers differ by cond(A) x eps."""
+    Pm = np.asarray(R.P_matrix(m.H_1, m.H_1))
+    Pi = np.asarray(R.P_inv_matrix(m))
+    x = np.einsum("ik,abk->abi", np.linalg.inv(Pm), psi[1:-1, 1:-1, :, 0])
+    zt = np.einsum("ik,abk->abi", Pi, zeta[1:-1, 1:-1, :, 0])
+    out = []
+    for i, A in enumerate((R._pin_first(-R.construct_spA(m.M, m.P, m.dx, 0.0)),
+                           -R.construct_spA(m.M, m.P, m.dx, R.S_eig(m)))):
+        b = -R._vec(zt[:, :, i])
+        if i == 0:
+            b[0] = 0
+        out.append(float(np.linalg.norm(A @ R._vec(x[:, :, i]) - b) / np.linalg.norm(b)))
+    return out
+
+
 @pytest.fixture(scope="module")
 def env():
     import torch
@@ -74,15 +93,17 @@ def test_reference_benchmark_sweep_sizes(env, M):
 
 def test_generic_rows_wide(env):
     """Wide generic rows on rectangular slabs: M = 2000 and 3000 (mixed-radix passes), 1999
-    (prime: direct DFT); non-power-of-two M above the split limit (8192) refused."""
+    (prime: direct DFT); rows the spectral solver cannot take refused: odd M above 8192 and
+    any M above 16384."""
     qg, O, R = env
     for M in (2000, 1999, 3000):
         st = qg.run_model_no_output(qg.bench_model(M, P=24, dt=600.0), nsteps=3)
         ref = O.State(R.bench_model(M, P=24, dt=600.0)).run(3)
         assert rel(st.to_numpy("psi"), ref.psi) < TOL, M
-    with pytest.raises(qg.QGError) as e:
-        qg.State(qg.bench_model(8200, P=8))
-    assert e.value.status == -2
+    for M in (8201, 16386):
+        with pytest.raises(qg.QGError) as e:
+            qg.State(qg.bench_model(M, P=8))
+        assert e.value.status == -2, M
 
 
 @pytest.mark.parametrize("M,P,steps", [(3328, 32, 3), (5000, 32, 3), (6000, 24, 3), (8191, 16, 2), (4001, 20, 2)])
@@ -126,6 +147,48 @@ def test_split_rows_f32(env):
     a = qg.run_model_no_output(m, nsteps=3)
     b = qg.run_model_no_output(m, nsteps=3, dtype=torch.float32)
     assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 5e-3
+
+
+@pytest.mark.parametrize("M,P,steps", [(16384, 64, 3), (16384, 32, 2), (16384, 16, 3), (8200, 8, 2), (9000, 4, 2)])
+def test_wide_split_rows(env, M, P, steps):
+    """Even rows wider than 8192 (8192 < M <= 16384): spec_fft_wide, each real row of the
+    pass-A/pass-B pipeline as a half-length complex DFT in LDS (H = M/2: 8192 = 2^13,
+    4100 = 4 5^2 41, 4500 = 4 3^2 5^3) plus the real split step, both systems of a workgroup
+    in turn.  The reference factors any M x P (laplacian.jl:60-75).  (The oracle's direct DFT
+    of a non-power-of-two row costs O(M^2) per row: small P there.)
+
+    Tolerance: the pinned Poisson system's condition number grows like M^2 (lowest x mode,
+    (2 pi / M)^2 against 8), so at 16384 two exact solvers -- device and oracle -- differ by
+    1e-10..7e-10 (measured: 2.4e-10 at P = 64, 1.3e-10 at 32, 7.0e-10 at 16; 9000 x 4:
+    1.8e-10).  Both are checked for exactness directly: the device solution's residuals in
+    the two modal systems must be at roundoff (< 1e-13, like the oracle's), and the two
+    solutions agree to 2e-9."""
+    qg, O, R = env
+    st = qg.run_model_no_output(qg.bench_model(M, P=P, dt=60.0), nsteps=steps)
+    ref = O.State(R.bench_model(M, P=P, dt=60.0)).run(steps)
+    m = R.bench_model(M, P=P, dt=60.0)
+    res_dev = modal_residuals(R, m, st.to_numpy("zeta"), st.to_numpy("psi"))
+    res_ref = modal_residuals(R, m, ref.zeta, ref.psi)
+    print(f"M={M} P={P} residuals device {res_dev} oracle {res_ref}")
+    assert max(res_dev) < 1e-13 and max(res_ref) < 1e-13, (res_dev, res_ref)
+    assert rel(st.to_numpy("zeta"), ref.zeta) < TOL
+    assert rel(st.to_numpy("psi"), ref.psi) < 2e-9
+    if M == 16384 and P == 16:  # PCG with the wide split solve as its preconditioner
+        pc = qg.run_model_no_output(qg.bench_model(M, P=P, dt=60.0), nsteps=steps, solver=1)
+        assert max(modal_residuals(R, m, pc.to_numpy("zeta"), pc.to_numpy("psi"))) < 1e-13
+        assert rel(pc.to_numpy("psi"), ref.psi) < 2e-9
+
+
+def test_wide_split_rows_f32(env):
+    """F32 state through the wide split (M = 16384): psi within the white-noise F32 bar of
+    DESIGN.md section 4 (2e-2: psi = A^-1 zeta amplifies zeta's F32 rounding in the gravest
+    modes by up to (M / 2 pi)^2; measured 1.0e-2 here)."""
+    import torch
+    qg, O, R = env
+    m = qg.bench_model(16384, P=32, dt=60.0)
+    a = qg.run_model_no_output(m, nsteps=3)
+    b = qg.run_model_no_output(m, nsteps=3, dtype=torch.float32)
+    assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 2e-2
 
 
 def test_invalid_arguments_are_refused(env):

@@ -73,7 +73,7 @@ def _worker(rank, world, port, M, P, steps, outdir, solver=0, resume_at=0, wind=
                           (2, 64, 64, 6, 1, 0, None), (4, 32, 64, 4, 1, 0, None), (2, 64, 64, 7, 0, 3, None), (2, 48, 64, 4, 0, 0, None), (2, 45, 32, 4, 0, 0, None),
                           (2, 8192, 32, 3, 0, 0, None), (2, 64, 64, 6, 0, 4, (0.1, 1000.0)), (4, 32, 64, 5, 0, 0, (0.1, 1000.0)),
                           (8, 64, 64, 4, 0, 0, None), (8, 32, 128, 3, 1, 0, None), (8, 1024, 64, 3, 0, 0, None),
-                          (2, 5000, 32, 3, 0, 0, None)])
+                          (2, 5000, 32, 3, 0, 0, None), (2, 16384, 32, 3, 0, 0, None)])
 def test_slabs_match_single_gpu(world, M, P, steps, solver, resume_at, wind):
     """solver 0 = spectral (record all-gather), 1 = PCG with the spectral preconditioner
     (its dot products and the z halo also cross the slabs).  resume_at > 0: every rank
