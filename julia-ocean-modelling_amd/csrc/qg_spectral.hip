@@ -3,6 +3,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "qg_fft.hpp"
@@ -1891,39 +1892,109 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
 // i W^-k (X_k - conj X_{H-k}).  The inverse keeps system 0's values in registers while system
 // 1 is transformed, then back-projects and stores both.  U, the recurrences, the carries and
 // the closure are the split path's.  A capability path (the reference factors any M x P).
-template <class S, bool INV>
-__global__ __launch_bounds__(SPL_T) void spec_fft_wide(SpecArgs a) {
+// POW2 (M = 16384): the half-length transform is the tuned 8192-point Stockham plan of the
+// power-of-two passes, in place in one LDS buffer with its twiddles in LDS, natural order
+// out; otherwise the planned mixed-radix DIF transform (global twiddles, digit-reversed out).
+// (1024 threads: one radix-8 butterfly per thread and pass, and the inverse's held system-0
+// values take 32 registers instead of 64: no spill at the 128-register cap)
+constexpr int WIDE_T = 1024;
+#ifndef QG_WIDE_FT
+#define QG_WIDE_FT 1024
+#endif
+#ifndef QG_WIDE_PF
+#define QG_WIDE_PF 0
+#endif
+constexpr int WIDE_FT = QG_WIDE_FT;  // forward transform threads
+using WPlan = FftPlan<SPL_MMAX, WIDE_T>;
+static_assert(!WPlan::PINGPONG && !FftPlan<SPL_MMAX, WIDE_FT>::PINGPONG, "the 8192-point plan runs in place");
+static_assert(FftPlan<SPL_MMAX, WIDE_FT>::LDS == WPlan::LDS, "one LDS size for both directions");
+template <class S, bool INV, bool POW2, int WT = POW2 ? (INV ? WIDE_T : WIDE_FT) : SPL_T>
+__global__ __launch_bounds__(WT) void spec_fft_wide(SpecArgs a) {
     using US = typename Store<S>::C;
-    const int M = (int)a.M, H = M / 2, t = threadIdx.x;
+    const int M = POW2 ? 2 * SPL_MMAX : (int)a.M, H = M / 2, t = threadIdx.x;
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
     const double2 *twM = a.tw, *twH = a.tw2;
     extern __shared__ double2 buf[];
-    __shared__ double pinw[SPL_T / 64];
-    constexpr int PER = SPL_MMAX / SPL_T;  // z values per thread (H <= SPL_MMAX)
-    auto Zat = [&](int k) { return buf[a.nrad ? a.perm[k] : k]; };
+    __shared__ double pinw[WT / 64];
+    constexpr int PER = SPL_MMAX / WT;  // z values per thread (H <= SPL_MMAX)
+    double2 *twl = buf + LdsSize<SPL_MMAX>::value;  // (POW2)
+    auto Zat = [&](int k) {
+        if constexpr (POW2) return buf[k];
+        else return buf[a.nrad ? a.perm[k] : k];
+    };
+    auto xform = [&](auto inv) {
+        constexpr bool I = decltype(inv)::value;
+        if constexpr (POW2) {
+            double2 unused[FftPlan<SPL_MMAX, WT>::R_LAST];
+            FftFromLds<SPL_MMAX, WT, I, false>::run(buf, buf, twl, unused);
+        } else {
+            spl_fft<I>(buf, a, twH, H);
+        }
+    };
+    if constexpr (POW2) fft_init_twiddles<SPL_MMAX, WT>(twl, twH);  // (published by the first row's barrier)
     double pin = 0;
     if constexpr (INV) {
-        const double pinp = a.pinned0 ? pin_part<SPL_T>(a, t) : 0.0;
-        pin = pin_total<SPL_T>(pinp, pinw);
+        const double pinp = a.pinned0 ? pin_part<WT>(a, t) : 0.0;
+        pin = pin_total<WT>(pinp, pinw);
         if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
+    }
+    // POW2: the row's raw values (x1[2n], x1[2n+1], x2[2n], x2[2n+1], n = t + p WT) are loaded
+    // once for both systems, and for F32 states the next row's are in flight across this row's
+    // two transforms (kept in the storage type until used: see spec_passB)
+    constexpr bool RAW = POW2 && !INV;
+    constexpr bool WPF = RAW && QG_WIDE_PF && sizeof(S) == 4;
+    S raw[RAW ? PER : 1][4], nxt[WPF ? PER : 1][4];
+    auto load_raw = [&](int64_t j, S (&d)[RAW ? PER : 1][4]) {
+        if constexpr (RAW) {
+            const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
+            const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
+#pragma unroll
+            for (int p = 0; p < PER; ++p) {
+                const int n = t + p * WT;
+                d[p][0] = r1[2 * n];
+                d[p][1] = r1[2 * n + 1];
+                d[p][2] = r2[2 * n];
+                d[p][3] = r2[2 * n + 1];
+            }
+        }
+    };
+    if constexpr (WPF) {
+        if ((int64_t)blockIdx.x < Pl) load_raw(blockIdx.x, nxt);
     }
     for (int64_t j = blockIdx.x; j < Pl; j += gridDim.x) {
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
         if constexpr (!INV) {
             const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
             const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
+            if constexpr (WPF) {
+#pragma unroll
+                for (int p = 0; p < PER; ++p)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) raw[p][q] = nxt[p][q];
+                if (j + gridDim.x < Pl) load_raw(j + gridDim.x, nxt);
+            } else if constexpr (RAW) {
+                load_raw(j, raw);
+            }
+#pragma unroll 1
             for (int s = 0; s < 2; ++s) {
                 const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];
-                for (int n = t; n < H; n += SPL_T) {
-                    const double xa = pa * (double)r1[2 * n] + pb * (double)r2[2 * n];
-                    const double xb = pa * (double)r1[2 * n + 1] + pb * (double)r2[2 * n + 1];
-                    buf[n] = make_double2(xa, xb);
+                if constexpr (RAW) {
+#pragma unroll
+                    for (int p = 0; p < PER; ++p)
+                        buf[t + p * WT] = make_double2(pa * (double)raw[p][0] + pb * (double)raw[p][2],
+                                                       pa * (double)raw[p][1] + pb * (double)raw[p][3]);
+                } else {
+                    for (int n = t; n < H; n += WT) {
+                        const double xa = pa * (double)r1[2 * n] + pb * (double)r2[2 * n];
+                        const double xb = pa * (double)r1[2 * n + 1] + pb * (double)r2[2 * n + 1];
+                        buf[n] = make_double2(xa, xb);
+                    }
                 }
                 __syncthreads();
-                spl_fft<false>(buf, a, twH, H);
+                xform(std::false_type{});
                 US *Us = Urow + (size_t)s * KS;
-                for (int k = t; k < H; k += SPL_T) {
+                for (int k = t; k < H; k += WT) {
                     const double2 Zk = Zat(k);
                     if (k == 0) {  // X_0 = Re + Im, X_H = Re - Im (both real)
                         Us[0] = Store<S>::c(make_double2(Zk.x + Zk.y, 0));
@@ -1938,10 +2009,11 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_wide(SpecArgs a) {
                 __syncthreads();  // the next transform overwrites buf
             }
         } else {
-            double2 z1[PER];  // system 0's z_n (n = t + p SPL_T), pin applied
+            double2 z1[PER];  // system 0's z_n (n = t + p WT), pin applied
+#pragma unroll 1
             for (int s = 0; s < 2; ++s) {
                 const US *Us = Urow + (size_t)s * KS;
-                for (int k = t; k < H; k += SPL_T) {
+                for (int k = t; k < H; k += WT) {
                     if (k == 0) {
                         const double X0 = d2(Us[0]).x, XH = d2(Us[H]).x;
                         buf[0] = make_double2(X0 + XH, X0 - XH);
@@ -1954,12 +2026,12 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_wide(SpecArgs a) {
                     }
                 }
                 __syncthreads();
-                spl_fft<true>(buf, a, twH, H);
+                xform(std::true_type{});
                 if (s == 0) {
                     const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
 #pragma unroll
                     for (int p = 0; p < PER; ++p) {
-                        const int n = t + p * SPL_T;
+                        const int n = t + p * WT;
                         if (n < H) {
                             const double2 z = Zat(n);
                             // the pinned unknown is exactly 0 (see spec_passB)
@@ -1975,7 +2047,7 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_wide(SpecArgs a) {
                     S *grow2 = out2 ? ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows) : nullptr;
 #pragma unroll
                     for (int p = 0; p < PER; ++p) {
-                        const int n = t + p * SPL_T;
+                        const int n = t + p * WT;
                         if (n < H) {
                             const double2 z2 = Zat(n);
                             const double x1a = z1[p].x, x1b = z1[p].y;
@@ -2109,19 +2181,23 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
     if (a.M > GEN_MMAX || std::getenv("QG_SPLIT_FORCE") != nullptr) {
         if (a.M > SPL_WMAX || (a.M > SPL_MMAX && a.M % 2 != 0)) return QG_ERR_UNSUPPORTED;
         const bool wsplit = a.M > SPL_MMAX;  // half-length transforms, one system at a time
-        const size_t lds = sizeof(double2) * (size_t)(wsplit ? a.M / 2 : a.M);
+        const bool wpow2 = a.M == 2 * SPL_MMAX;  // (the tuned 8192-point plan)
+        const size_t lds = sizeof(double2) * (wpow2 ? (size_t)WPlan::LDS : (size_t)(wsplit ? a.M / 2 : a.M));
         const unsigned rows = (unsigned)std::min<int64_t>(a.P, 1024);
         const dim3 rgrid((unsigned)a.Nc, (unsigned)((a.KH + SPL_KT - 1) / SPL_KT));
         auto fft = [&](const void *fn, auto kernel) -> int {
             QG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            kernel<<<rows, SPL_T, lds, s>>>(a);
+            kernel<<<rows, wpow2 ? (passB ? WIDE_T : WIDE_FT) : SPL_T, lds, s>>>(a);
             QG_LAUNCH_CHECK();
             return QG_OK;
         };
         if (!passB) {
-            if (wsplit)
-                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, false>, spec_fft_wide<float, false>)
-                               : fft((const void *)spec_fft_wide<double, false>, spec_fft_wide<double, false>));
+            if (wpow2)
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, false, true>, spec_fft_wide<float, false, true>)
+                               : fft((const void *)spec_fft_wide<double, false, true>, spec_fft_wide<double, false, true>));
+            else if (wsplit)
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, false, false>, spec_fft_wide<float, false, false>)
+                               : fft((const void *)spec_fft_wide<double, false, false>, spec_fft_wide<double, false, false>));
             else
                 QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, false>, spec_fft_split<float, false>)
                                : fft((const void *)spec_fft_split<double, false>, spec_fft_split<double, false>));
@@ -2132,9 +2208,12 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
             if (a.f32) spec_passB_split<float><<<rgrid, SPL_KT, 0, s>>>(a);
             else spec_passB_split<double><<<rgrid, SPL_KT, 0, s>>>(a);
             QG_LAUNCH_CHECK();
-            if (wsplit)
-                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, true>, spec_fft_wide<float, true>)
-                               : fft((const void *)spec_fft_wide<double, true>, spec_fft_wide<double, true>));
+            if (wpow2)
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, true, true>, spec_fft_wide<float, true, true>)
+                               : fft((const void *)spec_fft_wide<double, true, true>, spec_fft_wide<double, true, true>));
+            else if (wsplit)
+                QG_CHECK(a.f32 ? fft((const void *)spec_fft_wide<float, true, false>, spec_fft_wide<float, true, false>)
+                               : fft((const void *)spec_fft_wide<double, true, false>, spec_fft_wide<double, true, false>));
             else
                 QG_CHECK(a.f32 ? fft((const void *)spec_fft_split<float, true>, spec_fft_split<float, true>)
                                : fft((const void *)spec_fft_split<double, true>, spec_fft_split<double, true>));
