@@ -55,6 +55,23 @@ struct Store<float> {
     using C = float2;
     __device__ static C c(double2 v) { return make_float2((float)v.x, (float)v.y); }
 };
+// store of the spectral intermediate u (QG_NT_U: non-temporal, a tuning experiment)
+__device__ __forceinline__ void st_u(double2 *p, double2 v) {
+#ifdef QG_NT_U
+    typedef double V __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(V{v.x, v.y}, reinterpret_cast<V *>(p));
+#else
+    *p = v;
+#endif
+}
+__device__ __forceinline__ void st_u(float2 *p, float2 v) {
+#ifdef QG_NT_U
+    typedef float V __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(V{v.x, v.y}, reinterpret_cast<V *>(p));
+#else
+    *p = v;
+#endif
+}
 __device__ __forceinline__ double2 d2(double2 v) { return v; }
 __device__ __forceinline__ double2 d2(float2 v) { return make_double2(v.x, v.y); }
 
@@ -236,8 +253,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                         (void)o0;
                         u[q][s] = make_double2((r0 * a.csc) * B[s].x + r0 * u[q][s].x,
                                                (rN * a.csc) * B[s].y + rN * u[q][s].y);
-                        Urow[s * KS] = Store<S>::c(make_double2(u[q][s].x, 0));
-                        Urow[s * KS + NH] = Store<S>::c(make_double2(u[q][s].y, 0));
+                        st_u(Urow + s * KS, Store<S>::c(make_double2(u[q][s].x, 0)));
+                        st_u(Urow + s * KS + NH, Store<S>::c(make_double2(u[q][s].y, 0)));
                         bw[q][s] = make_double2(om[q][s].x * u[q][s].x + bw[q][s].x, om[q][s].y * u[q][s].y + bw[q][s].y);
                         om[q][s] = make_double2(om[q][s].x * r0, om[q][s].y * rN);
                     }
@@ -251,7 +268,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                         const double r = QG_PA_R(q, s, o);  // cs = r csc
                         (void)o;
                         u[q][s] = cfma(r, u[q][s], cscale(B[s], r * a.csc));
-                        Urow[s * KS + k] = Store<S>::c(u[q][s]);
+                        st_u(Urow + s * KS + k, Store<S>::c(u[q][s]));
                         bw[q][s] = cfma(om[q][s].x, u[q][s], bw[q][s]);
                         om[q][s].x *= r;
                     }
@@ -1097,8 +1114,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 const double r0 = cr[0], rN = cr[HN];
 #endif
                 u[q] = make_double2((r0 * csc) * X0 + r0 * u[q].x, (rN * csc) * XN + rN * u[q].y);
-                Urow[0] = Store<S>::c(make_double2(u[q].x, 0));
-                Urow[HN] = Store<S>::c(make_double2(u[q].y, 0));
+                st_u(Urow, Store<S>::c(make_double2(u[q].x, 0)));
+                st_u(Urow + HN, Store<S>::c(make_double2(u[q].y, 0)));
                 bw[q] = make_double2(om[q].x * u[q].x + bw[q].x, om[q].y * u[q].y + bw[q].y);
                 om[q] = make_double2(om[q].x * r0, om[q].y * rN);
             } else {
@@ -1113,7 +1130,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 const double r = cr[k];
 #endif
                 u[q] = cfma(r, u[q], cscale(X, r * csc));
-                Urow[k] = Store<S>::c(u[q]);
+                st_u(Urow + k, Store<S>::c(u[q]));
                 bw[q] = cfma(om[q].x, u[q], bw[q]);
                 om[q].x *= r;
             }
