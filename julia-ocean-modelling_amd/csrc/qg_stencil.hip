@@ -669,6 +669,9 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
                 if (layer == 0) last = Ut * (cdc * (Zw[1][w + 1] - Zw[1][w - 1]));
                 else last = rt * L0w[w];
                 T F = ((v_term - J_term) - beta_term) - last;
+#ifdef QG_EXP_NOARITH  // timing experiment only (wrong results): the loads and stores, no stencil
+                F = (((Zw[0][w] + Zw[2][w]) + (Sw[0][w] + Sw[2][w])) + ((Zw[1][w - 1] + Zw[1][w + 1]) + (Sw[1][w - 1] + Sw[1][w + 1]))) + ((L0w[w] + lm) + lp);
+#endif
                 if (layer == 0 && a.wind) F = F + (T)a.wind[j];  // wind extension (off: nullptr)
                 const T zcen = Zw[1][w];
                 const T g1 = v ? f1c.y : f1c.x, g2 = v ? f2c.y : f2c.x;
