@@ -193,8 +193,8 @@ def dropin_variant(qgamd, m, n, warmup, K, torch):
     del src
     return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K,
             "note": "reference array signatures from Python (ctypes per call), slot order kept on every "
-                    "call by an in-place history shift (2 slot copies per field per step, as "
-                    "store_new_state! copies)"}
+                    "call by an in-place history shift (store_new_state!'s 2 slot copies per field; "
+                    "f_store's done by the AB3 tendency as it reads F(t-1), F(t-2))"}
 
 
 # the JSON line's contract (the driver's fields + this bench's sub-records); checked before

@@ -88,6 +88,7 @@ struct qg_ctx {
     // (model.jl:102-106), by shifting the history slots in place before the new values are
     // written; the heads then stay 0
     bool keep_order = false;
+    bool no_fshift_fuse = std::getenv("QG_NO_FSHIFT_FUSE") != nullptr;  // (A/B: the separate shift)
     bool capturing = false;  // a step graph is being captured (no host reads, no polls)
     // deferred PCG: the latch is copied to page-locked memory every QG_PACE_STEPS steps and
     // read one interval later without blocking, so a failed certificate stops qg_step /
@@ -366,12 +367,17 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     int zh = c->heads[0], fh = c->heads[2], fh2 = (fh + 1) % 3;
     const int ph = c->heads[1];
     int zn = (zh + 2) % 3, fn = (fh + 2) % 3;
+    // keep_order, one rank, AB3: f_store's shift rides in the tendency (it reads F(t-1) and
+    // F(t-2) at every point anyway and writes them one slot down after reading, fshift1/2), so
+    // only zeta is shifted here -- zeta's slot 1 is read with a stencil and cannot be
+    // overwritten in place
+    const bool fuse_fshift = c->keep_order && !c->distributed && timestep >= 3 && !c->no_fshift_fuse;
     if (c->keep_order) {
         void *arr[2] = {c->zeta, c->fst};
-        QG_CHECK(launch_slot_shift(arr, 2, 2 * c->esize * c->F, c->stream));
+        QG_CHECK(launch_slot_shift(arr, fuse_fshift ? 1 : 2, 2 * c->esize * c->F, c->stream));
         zh = 1;
-        fh = 1;
-        fh2 = 2;
+        fh = fuse_fshift ? 0 : 1;
+        fh2 = fuse_fshift ? 1 : 2;
         zn = fn = 0;
     }
     TendArgsT<T> a{};
@@ -398,6 +404,10 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
         a.fprev2[l] = c->fieldt<T>(c->fst, l, fh2);
         a.zeta_out[l] = c->fieldt<T>(c->zeta, l, zn);
         a.f_out[l] = c->fieldt<T>(c->fst, l, fn);
+        if (fuse_fshift) {
+            a.fshift1[l] = c->fieldt<T>(c->fst, l, 1);
+            a.fshift2[l] = c->fieldt<T>(c->fst, l, 2);
+        }
     }
     if (!c->distributed) {
         for (int l = 0; l < 2; ++l) {

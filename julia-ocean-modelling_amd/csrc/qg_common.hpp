@@ -189,6 +189,11 @@ struct TendArgsT {
     const T *fprev2[2];
     T *zeta_out[2];
     T *f_out[2];
+    // store_new_state!'s shift of f_store fused into the AB3 step (keep-order drop-in, one
+    // rank): F(t-1) -> fshift1, F(t-2) -> fshift2 with their ghost images, point by point
+    // after they are read (fprev1 / fprev2 are then slots 1 / 2, f_out slot 1); nullptr: off
+    T *fshift1[2];
+    T *fshift2[2];
     RowSrcT<T> zeta_rows[2];
     RowSrcT<T> psi_rows[2];
     const double *wind;        // [P] upper-layer wind forcing per local row, or nullptr (off)

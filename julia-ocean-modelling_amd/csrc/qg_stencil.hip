@@ -361,6 +361,11 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
             const bool gr = a.write_ghost_rows;
             store_row_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
             store_row_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
+            if (ab3 && a.fshift1[layer]) {  // (see TendArgsT::fshift1)
+                T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
+                store_row_with_ghosts(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, i, f1c);
+                store_row_with_ghosts(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, i, f2c);
+            }
 #ifndef QG_CERT_NOWORK  // (timing experiment: the two-layer structure without the check)
             if constexpr (CERT) {  // this layer's parts of b_s and r_s at (i, j)
                 double part[4];
@@ -683,6 +688,13 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
                                    out_z[1], has_b);
             store_pair_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, xa, out_f[0],
                                    out_f[1], has_b);
+            if (ab3 && a.fshift1[layer]) {  // (see TendArgsT::fshift1)
+                T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
+                store_pair_with_ghosts(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, xa, f1c.x,
+                                       f1c.y, has_b);
+                store_pair_with_ghosts(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, xa, f2c.x,
+                                       f2c.y, has_b);
+            }
         }
     }
 }
@@ -877,10 +889,11 @@ __global__ __launch_bounds__(256) void tendency_direct_kernel(TendArgsT<T> a, in
     T F = ((v_term - J_term) - beta_term) - last;
     if (layer == 0 && a.wind) F = F + (T)a.wind[j];
     const T zcen = Z(0, 0);
-    T zn;
+    T zn, f1c = 0, f2c = 0;
     if (a.ab3) {
         const size_t o = (size_t)(j + 1) * ld + i + 1;
-        const T f1c = ld_stream(a.fprev1[layer] + o), f2c = ld_stream(a.fprev2[layer] + o);
+        f1c = ld_stream(a.fprev1[layer] + o);
+        f2c = ld_stream(a.fprev2[layer] + o);
         zn = zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * f1c)) + ((T)(5.0 / 12.0) * f2c));
     } else {
         zn = zcen + (dtT * F);
@@ -889,6 +902,11 @@ __global__ __launch_bounds__(256) void tendency_direct_kernel(TendArgsT<T> a, in
     const bool gr = a.write_ghost_rows;
     store_row_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
     store_row_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
+    if (a.ab3 && a.fshift1[layer]) {  // (see TendArgsT::fshift1)
+        T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
+        store_row_with_ghosts(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, i, f1c);
+        store_row_with_ghosts(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, i, f2c);
+    }
 }
 
 template <int TX, int PF, class T>

@@ -38,8 +38,11 @@ def _same(a, b):
         assert torch.equal(a[k], b[k]), k
 
 
+# (1280 x 1024: above the direct kernel's cut-off, so the LDS-ring tendency (F64), its
+# certifying two-layer form (PCG) and the pair kernel (F32) run with f_store's shift fused)
 @pytest.mark.parametrize("M,P,solver,f32", [(64, 48, 0, False), (128, 128, 1, False), (64, 64, 0, True),
-                                            (45, 30, 0, False)])
+                                            (45, 30, 0, False), (1280, 1024, 0, False), (1280, 1024, 1, False),
+                                            (1280, 1024, 0, True)])
 def test_keep_order_matches_rotation(qg, M, P, solver, f32):
     import torch
     m = qg.bench_model(M, P=P)
