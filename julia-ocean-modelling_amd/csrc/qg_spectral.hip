@@ -1063,7 +1063,15 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     const double *cr = a.cr + s * KS;
     const double csc = a.csc;
     // one row: consume the prefetched row (c1, c2), refill them with row jn (< s0: none)
+#ifdef QG_PHASE_TIMING  // diagnostic build: phase cycle counts of one workgroup's rows (printf)
+    const bool tim = wg == 0 && t == 0;
+    long long tp[5];
+#define QG_TP(n) if (tim) tp[n] = (long long)__builtin_readcyclecounter()
+#else
+#define QG_TP(n)
+#endif
     auto row_step = [&](int j, PV(&c1)[HK], PV(&c2)[HK], int jn) {
+        QG_TP(0);
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop
 #if defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)
         // two rows in flight: this row's r must be issued before the refill (loads complete
@@ -1091,11 +1099,30 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         }
 #else
         fft_pass<HN, HT, 1, 0, false, true, false>(nullptr, b0, twl, tt, in);
+        QG_TP(1);
+#if defined(QG_PAH_R_EARLY) && !defined(QG_PAH_PF2)
+        // this row's r ahead of the next row's loads: the recurrence's first use then waits
+        // only for these (loads complete in order), not for the whole prefetched row
+        double rq[HK], rNq = 0;
+#pragma unroll
+        for (int q = 0; q < HK; ++q) rq[q] = cr[t + q * HT];
+        if (t == 0) rNq = cr[HN];
+#endif
         if (jn >= s0) load_row(jn, c1, c2);
         {
             double2 dummy[HPlan::R_LAST];
             fft_run<HN, HT, HPlan::R0, 1, false, false>(b0, b1, twl, tt, dummy);
         }
+#endif
+        QG_TP(2);
+#if defined(QG_PAH_R_BATCH) && !defined(QG_PAH_PF2)
+        // this row's r loaded in one batch before the recurrence: one wait (which also covers
+        // the prefetched row, long landed by now), then the u stores flow -- a load inside the
+        // loop would wait for the previous line's store each time (vmcnt counts stores too)
+        double rq[HK], rNq = 0;
+#pragma unroll
+        for (int q = 0; q < HK; ++q) rq[q] = cr[t + q * HT];
+        if (t == 0) rNq = cr[HN];
 #endif
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
 #pragma unroll
@@ -1108,7 +1135,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                     dc += X0;
                     a.hline[j] = X0;
                 }
-#if defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)
+#if (defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)) || defined(QG_PAH_R_EARLY) || defined(QG_PAH_R_BATCH)
                 const double r0 = rq[q], rN = rNq;
 #else
                 const double r0 = cr[0], rN = cr[HN];
@@ -1124,7 +1151,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                 const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
                 const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
-#if defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)
+#if (defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)) || defined(QG_PAH_R_EARLY) || defined(QG_PAH_R_BATCH)
                 const double r = rq[q];
 #else
                 const double r = cr[k];
@@ -1135,7 +1162,14 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 om[q].x *= r;
             }
         }
+        QG_TP(3);
         if constexpr (Fwd::b0_read_late) __syncthreads();  // the next row's first pass writes b0
+#ifdef QG_PHASE_TIMING
+        QG_TP(4);
+        if (tim && j >= e - 6)
+            printf("passA_half row %d: pass1 %lld  fft %lld  split+rec %lld  tail %lld\n", j, tp[1] - tp[0],
+                   tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3]);
+#endif
     };
 #ifdef QG_PAH_PF2
     PV qf1[HK], qf2[HK];
