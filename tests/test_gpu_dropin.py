@@ -133,6 +133,22 @@ def test_graph_replay_certifies_each_solve_once(qg, monkeypatch):
     _same(_logical(st), _logical(ref))
 
 
+@pytest.mark.parametrize("M,solver", [(128, 0), (128, 1), (1280, 0)])
+def test_keep_order_graph_replay(qg, monkeypatch, M, solver):
+    """Keep-order stepping captured in HIP graphs (QG_GRAPH=1): the captured AB3 steps carry
+    the in-place shifts (f_store's inside the tendency on one rank) and replay to exactly the
+    rotating stream path's logical arrays."""
+    m = qg.bench_model(M, P=1024 if M > 1000 else None)
+    ref = qg.initialise_model(m, solver=solver)
+    ref.run(1, 25)
+    monkeypatch.setenv("QG_GRAPH", "1")
+    st = qg.initialise_model(m, solver=solver)
+    st.set_keep_order(True)
+    st.run(1, 25)
+    assert st.heads() == [0, 0, 0]
+    _same(_physical(st), _logical(ref))
+
+
 @pytest.mark.parametrize("f32", [False, True])
 def test_reference_signatures_keep_order_and_unbind(qg, f32):
     """evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(model, zeta, psi, P, H) on bare
