@@ -147,7 +147,9 @@ int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2
  * values after each qg_evolve_zeta / qg_evolve_psi, as the reference's copies leave them.
  * The history is shifted in place (slot 3 <- 2 <- 1: two slot copies per field, the
  * reference's own data movement) before the new values are written to slot 1, so the heads
- * stay 0 and no qg_canonicalize is needed.  on = 1 canonicalizes first.  For callers that
+ * stay 0 and no qg_canonicalize is needed; on one rank the AB3 tendency moves f_store's
+ * history itself as it reads it (each slot rewritten with its periodic ghost images).
+ * on = 1 canonicalizes first.  For callers that
  * hand the reference's arrays to every call (evolve_zeta!(model, zeta, psi, t, f_store));
  * qg_run is faster rotating (the default, on = 0).                                          */
 int qg_set_keep_order(qg_ctx *ctx, int on);

@@ -149,13 +149,15 @@ def test_split_rows_f32(env):
     assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 5e-3
 
 
-@pytest.mark.parametrize("M,P,steps", [(16384, 64, 3), (16384, 32, 2), (16384, 16, 3), (8200, 8, 2), (9000, 4, 2)])
-def test_wide_split_rows(env, M, P, steps):
+@pytest.mark.parametrize("M,P,steps,kw", [(16384, 64, 3, {}), (16384, 32, 2, {}), (16384, 16, 3, {}), (8200, 8, 2, {}),
+                                          (9000, 4, 2, {}), (16384, 9, 2, {}), (16384, 24, 2, {"chunk_rows": 8})])
+def test_wide_split_rows(env, M, P, steps, kw):
     """Even rows wider than 8192 (8192 < M <= 16384): spec_fft_wide, each real row of the
     pass-A/pass-B pipeline as a half-length complex DFT in LDS (H = M/2: 8192 = 2^13,
     4100 = 4 5^2 41, 4500 = 4 3^2 5^3) plus the real split step, both systems of a workgroup
     in turn.  The reference factors any M x P (laplacian.jl:60-75).  (The oracle's direct DFT
-    of a non-power-of-two row costs O(M^2) per row: small P there.)
+    of a non-power-of-two row costs O(M^2) per row: small P there.)  Odd P (one-row chunks)
+    and an explicit chunk size too.
 
     Tolerance: the pinned Poisson system's condition number grows like M^2 (lowest x mode,
     (2 pi / M)^2 against 8), so at 16384 two exact solvers -- device and oracle -- differ by
@@ -164,7 +166,7 @@ def test_wide_split_rows(env, M, P, steps):
     the two modal systems must be at roundoff (< 1e-13, like the oracle's), and the two
     solutions agree to 2e-9."""
     qg, O, R = env
-    st = qg.run_model_no_output(qg.bench_model(M, P=P, dt=60.0), nsteps=steps)
+    st = qg.run_model_no_output(qg.bench_model(M, P=P, dt=60.0), nsteps=steps, **kw)
     ref = O.State(R.bench_model(M, P=P, dt=60.0)).run(steps)
     m = R.bench_model(M, P=P, dt=60.0)
     res_dev = modal_residuals(R, m, st.to_numpy("zeta"), st.to_numpy("psi"))
