@@ -24,6 +24,12 @@ module QGMI355
 using AMDGPU
 
 const libqg = get(ENV, "QGMI355_LIB", joinpath(@__DIR__, "..", "lib", "libqgmi355.so"))
+const ABI_VERSION = 4  # QG_ABI_VERSION of include/qg_mi355.h this binding was written against
+
+function __init__()
+    v = ccall((:qg_abi_version, libqg), Cint, ())
+    v == ABI_VERSION || error("QGMI355: $(libqg) has C-ABI version $(v), this binding expects $(ABI_VERSION)")
+end
 
 # --- qg_params (include/qg_mi355.h), field order and padding identical to the C struct ----
 struct QGParams
@@ -222,6 +228,39 @@ end
 
 canonical!(s::QGState) = @qgcheck qg_canonicalize ccall((:qg_canonicalize, libqg), Cint, (Ptr{Cvoid},), s.ctx)
 
+"""`step!(s, t)`: one model step, the pair at run_model_no_output.jl:11-12 (`t` 1-based)."""
+step!(s::QGState, timestep::Integer) =
+    @qgcheck qg_step ccall((:qg_step, libqg), Cint, (Ptr{Cvoid}, Int64), s.ctx, timestep)
+
+"""`run!(s, first, n)`: `n` steps from `first`, the loop of run_model_no_output.jl:10-13."""
+run!(s::QGState, first::Integer, nsteps::Integer) =
+    @qgcheck qg_run ccall((:qg_run, libqg), Cint, (Ptr{Cvoid}, Int64, Int64), s.ctx, first, nsteps)
+
+"""`physical_slot(s, which, logical)`: where logical slot 1..3 of zeta (0) / psi (1) /
+f_store (2) sits in the rotating layout (0-based physical slot)."""
+function physical_slot(s::QGState, which::Integer, logical::Integer)
+    r = Ref{Cint}(0)
+    @qgcheck qg_slot ccall((:qg_slot, libqg), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{Cint}), s.ctx, which, logical, r)
+    Int(r[])
+end
+
+"""`pcg_certificate(s)`: the deferred PCG certificates so far (solves, failures, first failing
+solve, worst relative residual); QG_SOLVER_PCG only."""
+function pcg_certificate(s::QGState)
+    n, f, ff, w = Ref{Int64}(0), Ref{Int64}(0), Ref{Int64}(0), Ref{Float64}(0)
+    @qgcheck qg_pcg_certificate ccall((:qg_pcg_certificate, libqg), Cint,
+        (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}), s.ctx, n, f, ff, w)
+    (solves=n[], failures=f[], first_failure=ff[], worst_relres=w[])
+end
+
+"""`set_pcg_sync!(s, on)`: host-checked PCG (every residual read, general iteration on a
+failed certificate) instead of the deferred on-device certificate."""
+set_pcg_sync!(s::QGState, on::Bool=true) =
+    @qgcheck qg_set_pcg_sync ccall((:qg_set_pcg_sync, libqg), Cint, (Ptr{Cvoid}, Cint), s.ctx, Cint(on))
+
+"""`synchronize(s)`: wait for the context's queued work (bounded with a transport attached)."""
+synchronize(s::QGState) = @qgcheck qg_synchronize ccall((:qg_synchronize, libqg), Cint, (Ptr{Cvoid},), s.ctx)
+
 function stats(s::QGState)
     r = Ref{QGStats}()
     @qgcheck qg_get_stats ccall((:qg_get_stats, libqg), Cint, (Ptr{Cvoid}, Ptr{QGStats}), s.ctx, r)
@@ -362,5 +401,18 @@ end
 comm_init!(s::QGState, nranks::Integer, rank::Integer, id::Vector{UInt8}) =
     @qgcheck qg_comm_init ccall((:qg_comm_init, libqg), Cint, (Ptr{Cvoid}, Cint, Cint, Ptr{UInt8}),
                                 s.ctx, nranks, rank, id)
+
+"""`comm_set_timeout!(s, seconds)`: bound on every host wait of a multi-rank context."""
+comm_set_timeout!(s::QGState, seconds::Real) =
+    @qgcheck qg_comm_set_timeout ccall((:qg_comm_set_timeout, libqg), Cint, (Ptr{Cvoid}, Float64),
+                                       s.ctx, Float64(seconds))
+
+"""`comm_probe(s, reps)`: the step's halo exchange and record all-gather timed in isolation
+(ms each, and their bytes); every rank calls it."""
+function comm_probe(s::QGState, reps::Integer=20)
+    out = zeros(Float64, 4)
+    @qgcheck qg_comm_probe ccall((:qg_comm_probe, libqg), Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}), s.ctx, reps, out)
+    (halo_ms=out[1], halo_bytes=out[2], allgather_ms=out[3], allgather_bytes=out[4])
+end
 
 end # module
