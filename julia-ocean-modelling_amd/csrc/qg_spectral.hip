@@ -854,6 +854,20 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 #ifndef QG_COEF_LATE_B
     // the recurrence coefficients (r, 1/r) of the next row, loaded after this row's transform
     // (not live across it) so their L2 latency hides behind the stores
+#ifdef QG_PB_RINV  // experiment: r only from L2, 1/r formed in registers (half the table reads)
+    double crq1[KQ][2];
+    auto load_coef = [&]() {
+#pragma unroll
+        for (int q = 0; q < KQ; ++q)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int k = t + q * T;
+                if (NH % T == 0 || k < NH) crq1[q][s] = QG_CR(s * KS + k);
+            }
+    };
+    load_coef();
+#define QG_PB_R(q, s, o) make_double2(crq1[q][s], 1.0 / crq1[q][s])
+#else
     double2 crq[KQ][2];
     auto load_coef = [&]() {
 #pragma unroll
@@ -866,6 +880,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     };
     load_coef();
 #define QG_PB_R(q, s, o) crq[q][s]
+#endif
 #else
 #define QG_PB_R(q, s, o) QG_CRR(o)
 #endif
