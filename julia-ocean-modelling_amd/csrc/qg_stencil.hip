@@ -836,19 +836,13 @@ int launch_fill_ghost_cols(double *b, int64_t M, int64_t P, hipStream_t s) {
 // same order as tendency_kernel (lap at the five points, then the biharmonic), so the two
 // kernels are bit-identical.  Block: 64 x-points (one wave) x 4 rows.
 // ------------------------------------------------------------------------------------
+// one point (i, j) of one layer: loads, tendency, AB3 update, stores; returns the centre
+// values the certification uses (zeta, lap(psi), psi)
 template <class T>
-__global__ __launch_bounds__(256) void tendency_direct_kernel(TendArgsT<T> a, int nyA, int nyB) {
-    const TendBlock tb = tend_block();
-    const int layer = tb.z;
+__device__ __forceinline__ void direct_point(const TendArgsT<T> &a, int layer, int i, int j, T &zc_out, T &L0_out,
+                                             T &P0_out) {
     const int M = (int)a.M, P = (int)a.P;
     const int64_t ld = a.ld;
-    const int i = tb.x * 64 + (int)(threadIdx.x & 63);
-    const int w = (int)(threadIdx.x >> 6);
-    const int y = tb.y;
-    const bool second = y >= nyA;
-    const int r0 = second ? a.j2 : a.j0, r1 = second ? a.j3 : a.j1;
-    const int j = r0 + 4 * (second ? y - nyA : y) + w;
-    if (i >= M || j >= r1) return;  // no barriers below
     const T *psi = a.psi[layer], *zeta = a.zeta[layer];
     const RowSrcT<T> &prs = a.psi_rows[layer];
     const RowSrcT<T> &zrs = a.zeta_rows[layer];
@@ -906,6 +900,81 @@ __global__ __launch_bounds__(256) void tendency_direct_kernel(TendArgsT<T> a, in
         T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
         store_row_with_ghosts(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, i, f1c);
         store_row_with_ghosts(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, i, f2c);
+    }
+    zc_out = zcen;
+    L0_out = L0;
+    P0_out = S(0, 0);
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void tendency_direct_kernel(TendArgsT<T> a, int nyA, int nyB) {
+    const TendBlock tb = tend_block();
+    const int layer = tb.z;
+    const int M = (int)a.M;
+    const int i = tb.x * 64 + (int)(threadIdx.x & 63);
+    const int w = (int)(threadIdx.x >> 6);
+    const int y = tb.y;
+    const bool second = y >= nyA;
+    const int r0 = second ? a.j2 : a.j0, r1 = second ? a.j3 : a.j1;
+    const int j = r0 + 4 * (second ? y - nyA : y) + w;
+    if (i >= M || j >= r1) return;  // no barriers below
+    T zc, L0, P0;
+    direct_point(a, layer, i, j, zc, L0, P0);
+}
+
+// The certifying form of the cache-resident kernel (PCG, one rank, small grids): each thread
+// steps both layers of its point and forms the previous solve's residual terms there
+// (tendency_kernel<CERT>'s per-point parts, layer 0's first); (b,b), (r,r) per block.
+__global__ __launch_bounds__(256) void tendency_direct_cert_kernel(TendArgsT<double> a, int nyA, int nyB) {
+    const TendBlock tb = tend_block();
+    const int M = (int)a.M;
+    const int i = tb.x * 64 + (int)(threadIdx.x & 63);
+    const int w = (int)(threadIdx.x >> 6);
+    const int y = tb.y;
+    const bool second = y >= nyA;
+    const int r0 = second ? a.j2 : a.j0, r1 = second ? a.j3 : a.j1;
+    const int j = r0 + 4 * (second ? y - nyA : y) + w;
+    double cv[4] = {0, 0, 0, 0};
+    if (i < M && j < r1) {
+        double part[2][4];
+#pragma unroll
+        for (int layer = 0; layer < 2; ++layer) {
+            double zc, L0, P0;
+            direct_point(a, layer, i, j, zc, L0, P0);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const double b = -(a.cert_in[2 * s + layer] * zc);
+                part[layer][2 * s] = b;
+                part[layer][2 * s + 1] = b + a.cert_pinv[2 * s + layer] * (L0 + a.cert_alpha[s] * P0);
+            }
+        }
+        double bs[2], rs[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            bs[s] = part[0][2 * s] + part[1][2 * s];
+            rs[s] = part[0][2 * s + 1] + part[1][2 * s + 1];
+        }
+        if (a.cert_pin && i == 0 && j == 0) bs[0] = rs[0] = 0.0;  // identity row: b = x = 0
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            cv[2 * s] = bs[s] * bs[s];
+            cv[2 * s + 1] = rs[s] * rs[s];
+        }
+    }
+    // block sums, fixed order (wave shuffles, then the four wave totals in order)
+    __shared__ double sv[4][4];
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        double v = cv[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) sv[k][w] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const double v = ((sv[threadIdx.x][0] + sv[threadIdx.x][1]) + sv[threadIdx.x][2]) + sv[threadIdx.x][3];
+        a.cert[4 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = v;
     }
 }
 
@@ -1003,7 +1072,34 @@ static int launch_tendency_cert_t(const TendArgsT<double> &a, int *nblk, hipStre
     return QG_OK;
 }
 
+#ifndef QG_TEND_DIRECT_PTS
+#define QG_TEND_DIRECT_PTS 1.2e6  // up to ~1100^2 (tools/tend_direct.sh: 128^2 13.6 -> 7.4 us, 1024^2 33.2 -> 31.2; 1536^2 slower)
+#endif
+static int tend_direct_env();
+
+// below this many points per layer the certifying tendency is the cache-resident one-point
+// form (both layers per thread): 256^2 17.7 -> 13.9 us, 512^2 20.7 -> 18.7 us; at 1024^2 the
+// two-layer ring form is faster (40.6 vs 43.1 us), so the cut sits below the plain
+// tendency's QG_TEND_DIRECT_PTS (QG_CERT_RING=1: always the ring form)
+#ifndef QG_CERT_DIRECT_PTS
+#define QG_CERT_DIRECT_PTS 0.5e6
+#endif
 int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
+    const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
+    const int de = tend_direct_env();
+    static const bool ring_only = std::getenv("QG_CERT_RING") != nullptr;  // (A/B: the ring form)
+    if ((de == 1 || (de < 0 && pts < QG_CERT_DIRECT_PTS)) && !ring_only) {
+        const int nA = (a.j1 - a.j0 + 3) / 4, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + 3) / 4 : 0;
+        if (nA + nB == 0) {
+            *nblk = 0;
+            return QG_OK;
+        }
+        dim3 grid((unsigned)((a.M + 63) / 64), (unsigned)(nA + nB), 1);
+        tendency_direct_cert_kernel<<<grid, 256, 0, s>>>(a, nA, nB);
+        QG_LAUNCH_CHECK();
+        *nblk = (int)(grid.x * grid.y);
+        return QG_OK;
+    }
     static int tx = -1;
     if (tx < 0) {
         const char *e = std::getenv("QG_CERT_TX");
@@ -1089,9 +1185,6 @@ static int launch_tend_direct(const TendArgsT<T> &a, hipStream_t s) {
     return QG_OK;
 }
 
-#ifndef QG_TEND_DIRECT_PTS
-#define QG_TEND_DIRECT_PTS 1.2e6  // up to ~1100^2 (tools/tend_direct.sh: 128^2 13.6 -> 7.4 us, 1024^2 33.2 -> 31.2; 1536^2 slower)
-#endif
 // QG_TEND_DIRECT: 1 forces the cache-resident kernel, 0 the ring kernel; unset = by size
 static int tend_direct_env() {
     static int v = -2;

@@ -98,11 +98,12 @@ def test_alpha_iteration_path(env, monkeypatch):
     assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-10
 
 
-@pytest.mark.parametrize("N,steps", [(64, 9), (256, 7), (1024, 5)])
+@pytest.mark.parametrize("N,steps", [(64, 9), (256, 7), (1024, 5), (1280, 4)])
 def test_deferred_certificate_fused_in_tendency(env, N, steps):
     """Default (deferred) certification: no host read per step; on one GPU each solve's
-    5-point residual is checked inside the next step's tendency (both layers per workgroup)
-    and latched on the device.  psi, zeta, f_store are bit-identical to the host-checked form,
+    5-point residual is checked inside the next step's tendency (both layers per workgroup in
+    the LDS-ring form, 1280^2; both layers per thread in the cache-resident form below
+    1.2 M points) and latched on the device.  psi, zeta, f_store are bit-identical to the host-checked form,
     every solve is certified (the last one by the stand-alone pass at the read), and the
     latched residuals are at roundoff."""
     torch, qg, R, O = env
