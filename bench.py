@@ -230,7 +230,8 @@ def validate_record(out):
         for key, spec in (("comm", _COMM), ("overlap_ab", _OVERLAP_AB)):
             if key not in out:
                 raise ValueError(f"multi-GPU record: missing {key}")
-            if "error" not in out[key]:  # (a failed leg is reported, not silently dropped)
+            # (a failed leg is reported, not silently dropped; --comm-probe-reps 0 skips both)
+            if "error" not in out[key] and "skipped" not in out[key]:
                 need(out[key], spec, key)
     return True
 
@@ -507,6 +508,8 @@ def main():
         out["comm"] = comm
     if overlap_ab is not None:
         out["overlap_ab"] = overlap_ab
+    if args.comm_probe_reps <= 0 and (world > 1 or args.comm_self) and args.solver == "spectral":
+        out["comm"] = out["overlap_ab"] = {"skipped": "--comm-probe-reps 0"}
     if args.dropin_steps > 0 and world == 1 and args.solver == "spectral" and args.dtype == "f64" \
             and not args.comm_self:
         del st

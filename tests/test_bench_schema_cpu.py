@@ -68,3 +68,11 @@ def test_failed_leg_is_reported_not_dropped():
     r["comm"] = {"error": "QGError: qg_comm_probe failed (-6)"}
     r["overlap_ab"] = {"error": "skipped: the comm probe failed"}
     assert bench.validate_record(r)
+
+
+def test_skipped_comm_legs_are_marked():
+    """--comm-probe-reps 0 skips both multi-GPU legs; the record says so and stays valid."""
+    r = json.loads(open([p for p in _committed() if "rehearsal" in p][0]).read().strip().splitlines()[-1])
+    r = copy.deepcopy(r)
+    r["comm"] = r["overlap_ab"] = {"skipped": "--comm-probe-reps 0"}
+    assert bench.validate_record(r)
