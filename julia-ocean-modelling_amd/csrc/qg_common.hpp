@@ -51,23 +51,14 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 __device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
 __device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
 
-// Streaming accesses (read or written once per step): plain by default; the QG_NT_* builds
-// mark them non-temporal (tuning experiments, tools/buildexp.sh).
+// Streaming accesses (read or written once per step; non-temporal variants measured no gain).
 template <class T>
 __device__ __forceinline__ void st_stream(T *p, T v) {
-#ifdef QG_NT_STORE
-    __builtin_nontemporal_store(v, p);
-#else
     *p = v;
-#endif
 }
 template <class T>
 __device__ __forceinline__ T ld_stream(const T *p) {
-#ifdef QG_NT_LOAD
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 
 // Write v at interior (i, j) and at every ghost cell that is a periodic image of it
@@ -98,9 +89,6 @@ __device__ __forceinline__ void store_with_ghosts(T *out, int64_t ld, int64_t M,
 template <class T>
 __device__ __forceinline__ void store_row_with_ghosts(T *row, T *grow, int M, int i, T v) {
     st_stream(row + i + 1, v);
-#ifdef QG_EXP_NOGHOST  // timing experiment only (wrong results)
-    return;
-#endif
     if (i == M - 1) row[0] = v;
     if (i == 0) row[M + 1] = v;
     if (grow) {

@@ -11,13 +11,7 @@
 
 namespace qg {
 
-#ifndef QG_CARRY_WAVES
-#define QG_CARRY_WAVES 8
-#endif
-#ifndef QG_CARRY_KB
-#define QG_CARRY_KB 16
-#endif
-constexpr int CARRY_WAVES = QG_CARRY_WAVES;
+constexpr int CARRY_WAVES = 8;
 constexpr int PIN_THREADS = 256;
 __host__ __device__ inline int pin_kblocks(int KH) { return (2 * KH + PIN_THREADS - 1) / PIN_THREADS; }
 
@@ -26,12 +20,9 @@ struct Geo {
     // threads per row: N/8 (one radix-8 butterfly per thread and pass: 4 passes at N = 4096).
     // One workgroup per CU (two row buffers + twiddles = 154 KB of LDS at N = 4096);
     // registers capped at 512 / (T / 256) per lane so the whole workgroup stays resident.
-#ifndef QG_SPEC_TDIV
-#define QG_SPEC_TDIV 8
-#endif
     // (below N = 2048 the N/8 workgroup would be too small to keep a CU busy: N/4, <= 256)
     // (N = 8192: 1024 threads, registers capped at 128 -- some spill; capability, not speed)
-    static constexpr int T0 = N / QG_SPEC_TDIV >= 256 ? N / QG_SPEC_TDIV : (N / 4 < 256 ? N / 4 : 256);
+    static constexpr int T0 = N / 8 >= 256 ? N / 8 : (N / 4 < 256 ? N / 4 : 256);
     static constexpr int T = T0 < 64 ? 64 : (T0 > 1024 ? 1024 : T0);
     static constexpr int MINW = T / 256 < 1 ? 1 : T / 256;
     static constexpr int KH = N / 2 + 1;
@@ -55,22 +46,12 @@ struct Store<float> {
     using C = float2;
     __device__ static C c(double2 v) { return make_float2((float)v.x, (float)v.y); }
 };
-// store of the spectral intermediate u (QG_NT_U: non-temporal, a tuning experiment)
+// store of the spectral intermediate u
 __device__ __forceinline__ void st_u(double2 *p, double2 v) {
-#ifdef QG_NT_U
-    typedef double V __attribute__((ext_vector_type(2)));
-    __builtin_nontemporal_store(V{v.x, v.y}, reinterpret_cast<V *>(p));
-#else
     *p = v;
-#endif
 }
 __device__ __forceinline__ void st_u(float2 *p, float2 v) {
-#ifdef QG_NT_U
-    typedef float V __attribute__((ext_vector_type(2)));
-    __builtin_nontemporal_store(V{v.x, v.y}, reinterpret_cast<V *>(p));
-#else
     *p = v;
-#endif
 }
 __device__ __forceinline__ double2 d2(double2 v) { return v; }
 __device__ __forceinline__ double2 d2(float2 v) { return make_double2(v.x, v.y); }
@@ -79,17 +60,10 @@ __device__ __forceinline__ double2 cfma(double s, double2 x, double2 y) {  // s*
     return make_double2(s * x.x + y.x, s * x.y + y.y);
 }
 
-// coefficient loads of the power-of-two passes (QG_EXP_CONSTCOEF: timing experiment only,
-// constants instead of the per-row L1/L2 re-reads -- wrong results)
-#ifdef QG_EXP_CONSTCOEF
-#define QG_CRR(o) make_double2(0.5, 2.0)
-#define QG_CCS(o) 0.25
-#define QG_CR(o) 0.5
-#else
+// coefficient loads of the power-of-two passes
 #define QG_CRR(o) a.crr[o]
 #define QG_CCS(o) a.ccs[o]
 #define QG_CR(o) a.cr[o]
-#endif
 
 // ------------------------------------------------------------------------------------
 // pass A: project + row DFT + chunk-local backward filter (one workgroup per chunk)
@@ -110,19 +84,12 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     const double2 *Zb = RES_B1 ? b1 : b0;
     // set-up loads first (twiddles, r of the real line k = N/2 (see spec_passB), the first
     // row), their LDS writes after: one memory latency in front of the first row, not one per
-    // load (QG_PA_SERIAL_HEAD restores the serial head)
-#ifdef QG_PA_SERIAL_HEAD
-    fft_init_twiddles<N, T>(twl, a.tw);
-    __shared__ double crN[2];
-    if (threadIdx.x < 2) crN[threadIdx.x] = QG_CR(threadIdx.x * a.KS + NH);
-    __syncthreads();
-#else
+    // load
     TwFill<N, T> twf;
     fft_twiddle_load<N, T>(twf, a.tw);
     __shared__ double crN[2];
     double crv = 0;
     if (threadIdx.x < 2) crv = QG_CR(threadIdx.x * a.KS + NH);
-#endif
     const int t = threadIdx.x, c = blockIdx.x;
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
@@ -161,22 +128,10 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         }
     };
     constexpr bool PF = N < 8192;  // (N = 8192: no register prefetch, registers are short)
-#ifdef QG_PA_PF2
-    // two rows in flight (rows j-1 and j-2 while row j is transformed): two register sets
-    // used alternately, the row loop unrolled by two
-    constexpr int DEPTH = (PF && Plan::REG_IN) ? 2 : 1;
-#else
-    constexpr int DEPTH = 1;
-#endif
-    S qf1[EP], qf2[EP];
-#if !defined(QG_PA_COEF_ROW) && !defined(QG_PA_COEF_LATE) && !defined(QG_PA_PF2)
     // r of this thread's lines, loaded once: row-invariant, and at this kernel's register
     // budget (224 VGPRs before at 4096) the values fit without spilling, so no row reloads
-    // them from L2 (QG_PA_COEF_ROW: reload per row, the old form; below 1024 no gain measured)
+    // them from L2 (below 1024 no gain measured)
     constexpr bool COEF_HOIST = N >= 1024 && N <= 4096;
-#else
-    constexpr bool COEF_HOIST = false;
-#endif
     double rqh[KQ][2];
     if constexpr (COEF_HOIST) {
 #pragma unroll
@@ -187,7 +142,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                 rqh[q][s] = (NH % T == 0 || k < NH) ? QG_CR(s * KS + k) : 0.0;
             }
     }
-    // one row: consume the prefetched row (c1, c2), refill them with row j - DEPTH, transform,
+    // one row: consume the prefetched row (c1, c2), refill them with row j - 1, transform,
     // split, filter
     auto row_step = [&](int j, auto &c1, auto &c2) {
         if constexpr (!PF) load_into(j, c1, c2);
@@ -195,7 +150,6 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         // this row's r, issued ahead of the next row's prefetch: loads complete in order
         // (vmcnt), so r loaded after the prefetch would make the recurrence wait for the
         // whole next row
-#ifndef QG_PA_COEF_LATE
         double rq[KQ][2];
 #pragma unroll
         for (int q = 0; q < KQ; ++q)
@@ -206,24 +160,12 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                 else if (NH % T == 0 || k < NH) rq[q][s] = QG_CR(s * KS + k);
             }
 #define QG_PA_R(q, s, o) rq[q][s]
-#else
-#define QG_PA_R(q, s, o) QG_CR(o)
-#endif
         if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
             double2 in[Plan::R0];
 #pragma unroll
             for (int p = 0; p < EP; ++p) in[p] = make_double2(p0 * c1[p] + p1 * c2[p], p2 * c1[p] + p3 * c2[p]);
-            if (PF && j - DEPTH >= s0) load_into(j - DEPTH, c1, c2);
-#ifdef QG_EXP_NOFFT  // timing experiment only (wrong results): the row, untransformed
-            {
-                double2 *Zw = const_cast<double2 *>(Zb);
-#pragma unroll
-                for (int p = 0; p < EP; ++p) Zw[lay<Plan::LAST_NS>(t + p * T)] = in[p];
-                __syncthreads();
-            }
-#else
+            if (PF && j - 1 >= s0) load_into(j - 1, c1, c2);
             FwdReg::run(in, b0, b1, twl);
-#endif
         } else {
 #pragma unroll
             for (int p = 0; p < EP; ++p) {
@@ -278,27 +220,11 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         if constexpr (B0_LATE) __syncthreads();  // the next row's first pass overwrites b0
     };
 #undef QG_PA_R
-    if constexpr (DEPTH == 2) {
-        load_into(e, pf1, pf2);
-        if (e - 1 >= s0) load_into(e - 1, qf1, qf2);
-#ifndef QG_PA_SERIAL_HEAD
-        fft_twiddle_store<N, T>(twl, twf);
-        if (threadIdx.x < 2) crN[threadIdx.x] = crv;
-        __syncthreads();
-#endif
-        for (int j = e; j >= s0; j -= 2) {
-            row_step(j, pf1, pf2);
-            if (j - 1 >= s0) row_step(j - 1, qf1, qf2);
-        }
-    } else {
-        if constexpr (PF) load_into(e, pf1, pf2);
-#ifndef QG_PA_SERIAL_HEAD
-        fft_twiddle_store<N, T>(twl, twf);
-        if (threadIdx.x < 2) crN[threadIdx.x] = crv;
-        __syncthreads();
-#endif
-        for (int j = e; j >= s0; --j) row_step(j, pf1, pf2);
-    }
+    if constexpr (PF) load_into(e, pf1, pf2);
+    fft_twiddle_store<N, T>(twl, twf);
+    if (threadIdx.x < 2) crN[threadIdx.x] = crv;
+    __syncthreads();
+    for (int j = e; j >= s0; --j) row_step(j, pf1, pf2);
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
         const int k = t + q * T;
@@ -501,7 +427,7 @@ __device__ __forceinline__ void carry_in(const SpecArgs &a, const Coef &cf, int 
 //   v_c = ULS_c + q v_{c+1}, v_Nc = 0      UIN_c = v_{c+1},  AU = v_0
 //   w_c = (WLS_c + gam UIN_c) + q w_{c-1}   WIN_c = w_{c-1},  AW = w_{Nc-1}
 // ------------------------------------------------------------------------------------
-constexpr int CARRY_KB = QG_CARRY_KB;
+constexpr int CARRY_KB = 16;
 constexpr int CARRY_SEG = CARRY_WAVES * (64 / CARRY_KB);
 constexpr int CARRY_REG = 8;  // chunks per segment held in registers
 
@@ -746,10 +672,6 @@ __device__ __forceinline__ double pin_total(double p, double *pinw) {
 
 __device__ __forceinline__ void chunk_carry(const SpecArgs &a, int s, int k, int c, double delta, bool inject,
                                             double2 &cu, double2 &w) {
-#ifdef QG_EXP_NOPROLOGUE  // timing experiment only (wrong results)
-    cu = w = make_double2(0, 0);
-    return;
-#endif
     const size_t o = ((size_t)c * 2 + s) * a.KS + k;
     const Coef cf = a.coef[s * a.KS + k];
     const double2 Ue = a.EXT[(size_t)s * a.KS + k], We = a.EXT[(size_t)(2 + s) * a.KS + k];
@@ -768,14 +690,10 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
     const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
     // set-up loads (twiddles, the chunk's singular-line values, (r, 1/r) of k = N/2) go out
-    // first and reach LDS just before pin_total's barrier (QG_PB_SERIAL_HEAD: the serial head,
+    // first and reach LDS just before pin_total's barrier (a serial head would put
     // one memory latency per load in front of the first row's loads)
-#ifdef QG_PB_SERIAL_HEAD
-    fft_init_twiddles<N, T>(twl, a.tw);
-#else
     TwFill<N, T> twf;
     fft_twiddle_load<N, T>(twf, a.tw);
-#endif
     const int t = threadIdx.x, c = blockIdx.x;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     // the chunk's values of the singular line, staged once (a global load per row would sit
@@ -786,15 +704,10 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     // that owns slot (0, 0), whose global load there would wait (in-order vmcnt) for the
     // next row's prefetch, and the whole workgroup for that wave at the next barrier
     __shared__ double2 crN[2];
-#ifdef QG_PB_SERIAL_HEAD
-    if (a.pinned0 && t < L) lline[t] = a.line[s0 + t];
-    if (N < 4096 && t < 2) crN[t] = QG_CRR(t * a.KS + NH);
-#else
     double llv = 0;
     double2 crv = make_double2(0, 0);
     if (a.pinned0 && t < L) llv = a.line[s0 + t];
     if (N < 4096 && t < 2) crv = QG_CRR(t * a.KS + NH);
-#endif
     const double pinp = a.pinned0 ? pin_part<T>(a, t) : 0.0;  // (lline, twl: see pin_total)
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
@@ -851,23 +764,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
             }
         }
     }
-#ifndef QG_COEF_LATE_B
     // the recurrence coefficients (r, 1/r) of the next row, loaded after this row's transform
     // (not live across it) so their L2 latency hides behind the stores
-#ifdef QG_PB_RINV  // experiment: r only from L2, 1/r formed in registers (half the table reads)
-    double crq1[KQ][2];
-    auto load_coef = [&]() {
-#pragma unroll
-        for (int q = 0; q < KQ; ++q)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int k = t + q * T;
-                if (NH % T == 0 || k < NH) crq1[q][s] = QG_CR(s * KS + k);
-            }
-    };
-    load_coef();
-#define QG_PB_R(q, s, o) make_double2(crq1[q][s], 1.0 / crq1[q][s])
-#else
     double2 crq[KQ][2];
     auto load_coef = [&]() {
 #pragma unroll
@@ -880,18 +778,12 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     };
     load_coef();
 #define QG_PB_R(q, s, o) crq[q][s]
-#endif
-#else
-#define QG_PB_R(q, s, o) QG_CRR(o)
-#endif
     // folded after the chunk set-up, so the carries' loads are not queued behind the pin
     // parts' (folding first: 4096^2 pass B 125.9 -> 137.9 us); its barrier also publishes
     // lline and the twiddles
-#ifndef QG_PB_SERIAL_HEAD
     fft_twiddle_store<N, T>(twl, twf);
     if (a.pinned0 && t < L) lline[t] = llv;
     if (N < 4096 && t < 2) crN[t] = crv;
-#endif
     const double pin = pin_total<T>(pinp, pinw);
     if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     for (int j = s0; j <= e; ++j) {
@@ -949,14 +841,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         }
         __syncthreads();
         double2 xo[Plan::R_LAST];  // last FFT pass output in registers: element t + r*T
-#ifdef QG_EXP_NOFFT
-        if constexpr (Plan::REG_OUT) {
-#pragma unroll
-            for (int p = 0; p < Plan::R_LAST; ++p) xo[p] = b0[t + p * T];
-        }
-#else
         Inv::run(b0, b1, twl, xo);
-#endif
         S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
         S *row1 = out1 + (size_t)(j + 1) * ld;
         const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
@@ -977,10 +862,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                 if (row2) store_row_with_ghosts(row2, grow2, N, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
             }
         }
-#ifndef QG_COEF_LATE_B
         asm volatile("" ::: "memory");
         if (j < e) load_coef();
-#endif
         if constexpr (Inv::b0_read_late) __syncthreads();  // the next row's recurrence writes b0
     }
 #undef QG_PB_R
@@ -1078,24 +961,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     const double *cr = a.cr + s * KS;
     const double csc = a.csc;
     // one row: consume the prefetched row (c1, c2), refill them with row jn (< s0: none)
-#ifdef QG_PHASE_TIMING  // diagnostic build: phase cycle counts of one workgroup's rows (printf)
-    const bool tim = wg == 0 && t == 0;
-    long long tp[5];
-#define QG_TP(n) if (tim) tp[n] = (long long)__builtin_readcyclecounter()
-#else
-#define QG_TP(n)
-#endif
     auto row_step = [&](int j, PV(&c1)[HK], PV(&c2)[HK], int jn) {
-        QG_TP(0);
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop
-#if defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)
-        // two rows in flight: this row's r must be issued before the refill (loads complete
-        // in order, so a later r load would wait for both prefetched rows)
-        double rq[HK], rNq = 0;
-#pragma unroll
-        for (int q = 0; q < HK; ++q) rq[q] = cr[t + q * HT];
-        if (t == 0) rNq = cr[HN];
-#endif
         double2 in[HK];
 #pragma unroll
         for (int p = 0; p < HK; ++p)
@@ -1104,41 +971,12 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         // first pass from registers, then the next row's loads (in[] is dead by then: fewer
         // live registers than loading first), then the remaining passes
         const int tt = opaque_tid();
-#ifdef QG_EXP_NOFFT  // timing experiment only (wrong results): the row, untransformed
-        {
-            double2 *Zw = const_cast<double2 *>(Zb);
-#pragma unroll
-            for (int p = 0; p < HK; ++p) Zw[lay<HPlan::LAST_NS>(t + p * HT)] = in[p];
-            if (jn >= s0) load_row(jn, c1, c2);
-            __syncthreads();
-        }
-#else
         fft_pass<HN, HT, 1, 0, false, true, false>(nullptr, b0, twl, tt, in);
-        QG_TP(1);
-#if defined(QG_PAH_R_EARLY) && !defined(QG_PAH_PF2)
-        // this row's r ahead of the next row's loads: the recurrence's first use then waits
-        // only for these (loads complete in order), not for the whole prefetched row
-        double rq[HK], rNq = 0;
-#pragma unroll
-        for (int q = 0; q < HK; ++q) rq[q] = cr[t + q * HT];
-        if (t == 0) rNq = cr[HN];
-#endif
         if (jn >= s0) load_row(jn, c1, c2);
         {
             double2 dummy[HPlan::R_LAST];
             fft_run<HN, HT, HPlan::R0, 1, false, false>(b0, b1, twl, tt, dummy);
         }
-#endif
-        QG_TP(2);
-#if defined(QG_PAH_R_BATCH) && !defined(QG_PAH_PF2)
-        // this row's r loaded in one batch before the recurrence: one wait (which also covers
-        // the prefetched row, long landed by now), then the u stores flow -- a load inside the
-        // loop would wait for the previous line's store each time (vmcnt counts stores too)
-        double rq[HK], rNq = 0;
-#pragma unroll
-        for (int q = 0; q < HK; ++q) rq[q] = cr[t + q * HT];
-        if (t == 0) rNq = cr[HN];
-#endif
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
@@ -1150,11 +988,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                     dc += X0;
                     a.hline[j] = X0;
                 }
-#if (defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)) || defined(QG_PAH_R_EARLY) || defined(QG_PAH_R_BATCH)
-                const double r0 = rq[q], rN = rNq;
-#else
                 const double r0 = cr[0], rN = cr[HN];
-#endif
                 u[q] = make_double2((r0 * csc) * X0 + r0 * u[q].x, (rN * csc) * XN + rN * u[q].y);
                 st_u(Urow, Store<S>::c(make_double2(u[q].x, 0)));
                 st_u(Urow + HN, Store<S>::c(make_double2(u[q].y, 0)));
@@ -1166,38 +1000,17 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                 const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
                 const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
-#if (defined(QG_PAH_PF2) && !defined(QG_PAH_LATE_R)) || defined(QG_PAH_R_EARLY) || defined(QG_PAH_R_BATCH)
-                const double r = rq[q];
-#else
                 const double r = cr[k];
-#endif
                 u[q] = cfma(r, u[q], cscale(X, r * csc));
                 st_u(Urow + k, Store<S>::c(u[q]));
                 bw[q] = cfma(om[q].x, u[q], bw[q]);
                 om[q].x *= r;
             }
         }
-        QG_TP(3);
         if constexpr (Fwd::b0_read_late) __syncthreads();  // the next row's first pass writes b0
-#ifdef QG_PHASE_TIMING
-        QG_TP(4);
-        if (tim && j >= e - 6)
-            printf("passA_half row %d: pass1 %lld  fft %lld  split+rec %lld  tail %lld\n", j, tp[1] - tp[0],
-                   tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3]);
-#endif
     };
-#ifdef QG_PAH_PF2
-    PV qf1[HK], qf2[HK];
-    load_row(e, pf1, pf2);
-    if (e - 1 >= s0) load_row(e - 1, qf1, qf2);
-    for (int j = e; j >= s0; j -= 2) {
-        row_step(j, pf1, pf2, j - 2);
-        if (j - 1 >= s0) row_step(j - 1, qf1, qf2, j - 3);
-    }
-#else
     load_row(e, pf1, pf2);
     for (int j = e; j >= s0; --j) row_step(j, pf1, pf2, j - 1);
-#endif
 #pragma unroll
     for (int q = 0; q < HK; ++q) {
         const int k = t + q * HT;
@@ -1347,17 +1160,6 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
         }
         // first inverse pass, then the next row's loads (in[] dead), then the remaining passes
         const int tt = opaque_tid();
-#ifdef QG_EXP_NOFFT  // timing experiment only (wrong results)
-        {
-            double2 *Xw = const_cast<double2 *>(Xb);
-            __syncthreads();  // (Xs = b1 may be Xb: every partner read above is done)
-#pragma unroll
-            for (int q = 0; q < HK; ++q) Xw[lay<HPlan::LAST_NS>(t + q * HT)] = in[q];
-            if (j < e) load_u(j + 1);
-            if constexpr (SYS == 1) load_y(j);
-            __syncthreads();
-        }
-#else
         fft_pass<HN, HT, 1, 0, true, true, false>(nullptr, b0, twl, tt, in);
         if (j < e) load_u(j + 1);
         if constexpr (SYS == 1) load_y(j);
@@ -1365,7 +1167,6 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
             double2 dummy[HPlan::R_LAST];
             fft_run<HN, HT, HPlan::R0, 1, true, false>(b0, b1, twl, tt, dummy);
         }
-#endif
         if constexpr (SYS == 0) {
             S *yr = static_cast<S *>(a.half_tmp) + (size_t)j * a.M;
             const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
@@ -1964,13 +1765,7 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
 // (1024 threads: one radix-8 butterfly per thread and pass, and the inverse's held system-0
 // values take 32 registers instead of 64: no spill at the 128-register cap)
 constexpr int WIDE_T = 1024;
-#ifndef QG_WIDE_FT
-#define QG_WIDE_FT 1024
-#endif
-#ifndef QG_WIDE_PF
-#define QG_WIDE_PF 0
-#endif
-constexpr int WIDE_FT = QG_WIDE_FT;  // forward transform threads
+constexpr int WIDE_FT = 1024;  // forward transform threads (512 measured slower)
 using WPlan = FftPlan<SPL_MMAX, WIDE_T>;
 static_assert(!WPlan::PINGPONG && !FftPlan<SPL_MMAX, WIDE_FT>::PINGPONG, "the 8192-point plan runs in place");
 static_assert(FftPlan<SPL_MMAX, WIDE_FT>::LDS == WPlan::LDS, "one LDS size for both directions");
@@ -2006,11 +1801,9 @@ __global__ __launch_bounds__(WT) void spec_fft_wide(SpecArgs a) {
         if (blockIdx.x == 0 && t == 0) a.scal[1] = pin;
     }
     // POW2: the row's raw values (x1[2n], x1[2n+1], x2[2n], x2[2n+1], n = t + p WT) are loaded
-    // once for both systems, and for F32 states the next row's are in flight across this row's
-    // two transforms (kept in the storage type until used: see spec_passB)
+    // once for both systems (a next-row prefetch spilled at the 1024-thread register cap)
     constexpr bool RAW = POW2 && !INV;
-    constexpr bool WPF = RAW && QG_WIDE_PF && sizeof(S) == 4;
-    S raw[RAW ? PER : 1][4], nxt[WPF ? PER : 1][4];
+    S raw[RAW ? PER : 1][4];
     auto load_raw = [&](int64_t j, S (&d)[RAW ? PER : 1][4]) {
         if constexpr (RAW) {
             const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
@@ -2025,23 +1818,12 @@ __global__ __launch_bounds__(WT) void spec_fft_wide(SpecArgs a) {
             }
         }
     };
-    if constexpr (WPF) {
-        if ((int64_t)blockIdx.x < Pl) load_raw(blockIdx.x, nxt);
-    }
     for (int64_t j = blockIdx.x; j < Pl; j += gridDim.x) {
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
         if constexpr (!INV) {
             const S *r1 = static_cast<const S *>(a.in1) + fidx(1, j + 1, ld);
             const S *r2 = static_cast<const S *>(a.in2) + fidx(1, j + 1, ld);
-            if constexpr (WPF) {
-#pragma unroll
-                for (int p = 0; p < PER; ++p)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) raw[p][q] = nxt[p][q];
-                if (j + gridDim.x < Pl) load_raw(j + gridDim.x, nxt);
-            } else if constexpr (RAW) {
-                load_raw(j, raw);
-            }
+            if constexpr (RAW) load_raw(j, raw);
 #pragma unroll 1
             for (int s = 0; s < 2; ++s) {
                 const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];

@@ -96,13 +96,9 @@ struct TendBlock {
     int x, y, z;
 };
 __device__ __forceinline__ TendBlock tend_block() {
-#ifdef QG_TEND_NO_XCD
-    return {(int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z};
-#else
     const int b = xcd_logical_id();
     const int x = b % gridDim.x, r = b / gridDim.x;
     return {x, r % (int)gridDim.y, r / (int)gridDim.y};
-#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -248,19 +244,7 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
     // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 into LDS.  All eight rows' loads
     // are issued before the first LDS write (a fetch-commit loop waited one full memory latency
     // per row: eight round trips in front of every strip, while the workgroups of a chip-full,
-    // which start together, all sat in them); QG_TEND_SERIAL_PROLOGUE restores that order.
-#ifdef QG_TEND_SERIAL_PROLOGUE
-    for (int j = jb0 - 2; j <= jb0 + 2; ++j) {
-        T c = 0, h = 0;
-        fetch_psi(j, c, h);
-        commit_psi(j, c, h);
-    }
-    for (int j = jb0 - 1; j <= jb0 + 1; ++j) {
-        T c = 0, h = 0;
-        fetch_zeta(j, c, h);
-        commit_zeta(j, c, h);
-    }
-#else
+    // which start together, all sat in them).
     {
         T p0c[5], p0h[5], z0c[3], z0h[3];
 #pragma unroll
@@ -278,7 +262,6 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
 #pragma unroll
         for (int k = 0; k < 3; ++k) commit_zeta(jb0 - 1 + k, z0c[k], z0h[k]);
     }
-#endif
     // prefetch for iterations jb0 .. jb0+PF-1: psi row j+3, zeta row j+2 (committed while
     // rows are still needed, i.e. j+2 <= jb1) and F of row j
 #pragma unroll
@@ -303,12 +286,10 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
             commit_zeta(j + 2, zc[0], zh[0]);
         }
         const T f1c = f1[0], f2c = f2[0];
-#ifndef QG_TEND_LATE_F
         // land this row's F(t-1), F(t-2) (issued last iteration) before the next row's loads
         // go out: loads complete in order (vmcnt), and with f1c / f2c first read after the
         // new loads the compiler waited for those too (vmcnt(0)) on every row
         asm volatile("" : : "v"(f1c), "v"(f2c) : "memory");
-#endif
 #pragma unroll
         for (int k = 0; k + 1 < PF; ++k) {
             pc[k] = pc[k + 1];
@@ -366,7 +347,6 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
                 store_row_with_ghosts(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, i, f1c);
                 store_row_with_ghosts(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, i, f2c);
             }
-#ifndef QG_CERT_NOWORK  // (timing experiment: the two-layer structure without the check)
             if constexpr (CERT) {  // this layer's parts of b_s and r_s at (i, j)
                 double part[4];
 #pragma unroll
@@ -384,7 +364,6 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
                     pend_j = j;
                 }
             }
-#endif
         }
     }
     if constexpr (CERT) {
@@ -561,18 +540,6 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
 
     // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 into LDS, every load issued
     // before the first LDS write (see tendency_kernel)
-#ifdef QG_TEND_SERIAL_PROLOGUE
-    for (int j = jb0 - 2; j <= jb0 + 2; ++j) {
-        V c = {0, 0}, h = {0, 0};
-        fetch_psi(j, c, h);
-        commit(sp[ring(j, RP)], c, h);
-    }
-    for (int j = jb0 - 1; j <= jb0 + 1; ++j) {
-        V c = {0, 0}, h = {0, 0};
-        fetch_zeta(j, c, h);
-        commit(sz[ring(j, RZ)], c, h);
-    }
-#else
     {
         V p0c[5], p0h[5], z0c[3], z0h[3];
 #pragma unroll
@@ -590,7 +557,6 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
 #pragma unroll
         for (int k = 0; k < 3; ++k) commit(sz[ring(jb0 - 1 + k, RZ)], z0c[k], z0h[k]);
     }
-#endif
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         const int j = jb0 + k;
@@ -615,9 +581,7 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
             commit(sz[ring(j + 2, RZ)], zc[0], zh[0]);
         }
         const V f1c = f1[0], f2c = f2[0];
-#ifndef QG_TEND_LATE_F
         asm volatile("" : : "v"(f1c), "v"(f2c) : "memory");  // (see tendency_kernel)
-#endif
 #pragma unroll
         for (int k = 0; k + 1 < PF; ++k) {
             pc[k] = pc[k + 1];
@@ -674,9 +638,6 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
                 if (layer == 0) last = Ut * (cdc * (Zw[1][w + 1] - Zw[1][w - 1]));
                 else last = rt * L0w[w];
                 T F = ((v_term - J_term) - beta_term) - last;
-#ifdef QG_EXP_NOARITH  // timing experiment only (wrong results): the loads and stores, no stencil
-                F = (((Zw[0][w] + Zw[2][w]) + (Sw[0][w] + Sw[2][w])) + ((Zw[1][w - 1] + Zw[1][w + 1]) + (Sw[1][w - 1] + Sw[1][w + 1]))) + ((L0w[w] + lm) + lp);
-#endif
                 if (layer == 0 && a.wind) F = F + (T)a.wind[j];  // wind extension (off: nullptr)
                 const T zcen = Zw[1][w];
                 const T g1 = v ? f1c.y : f1c.x, g2 = v ? f2c.y : f2c.x;
@@ -994,10 +955,7 @@ static int launch_tend_variant(const TendArgsT<T> &a, int rows, hipStream_t s) {
 // 38 us.)
 template <class T>
 static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
-#ifndef QG_TEND_PF
-#define QG_TEND_PF 1
-#endif
-    constexpr int TX = 256, PF = QG_TEND_PF;  // register prefetch depth (rows)
+    constexpr int TX = 256, PF = 1;  // register prefetch depth (rows)
     static int slots[2] = {0, 0};  // per element type
     int &sl = slots[sizeof(T) == 4];
     if (sl == 0) {
@@ -1072,23 +1030,20 @@ static int launch_tendency_cert_t(const TendArgsT<double> &a, int *nblk, hipStre
     return QG_OK;
 }
 
-#ifndef QG_TEND_DIRECT_PTS
-#define QG_TEND_DIRECT_PTS 1.2e6  // up to ~1100^2 (tools/tend_direct.sh: 128^2 13.6 -> 7.4 us, 1024^2 33.2 -> 31.2; 1536^2 slower)
-#endif
+// up to ~1100^2 (128^2 13.6 -> 7.4 us, 1024^2 33.2 -> 31.2; 1536^2 slower)
+constexpr double TEND_DIRECT_PTS = 1.2e6;
 static int tend_direct_env();
 
 // below this many points per layer the certifying tendency is the cache-resident one-point
 // form (both layers per thread): 256^2 17.7 -> 13.9 us, 512^2 20.7 -> 18.7 us; at 1024^2 the
 // two-layer ring form is faster (40.6 vs 43.1 us), so the cut sits below the plain
-// tendency's QG_TEND_DIRECT_PTS (QG_CERT_RING=1: always the ring form)
-#ifndef QG_CERT_DIRECT_PTS
-#define QG_CERT_DIRECT_PTS 0.5e6
-#endif
+// tendency's TEND_DIRECT_PTS (QG_CERT_RING=1: always the ring form)
+constexpr double CERT_DIRECT_PTS = 0.5e6;
 int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
     const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
     const int de = tend_direct_env();
     static const bool ring_only = std::getenv("QG_CERT_RING") != nullptr;  // (A/B: the ring form)
-    if ((de == 1 || (de < 0 && pts < QG_CERT_DIRECT_PTS)) && !ring_only) {
+    if ((de == 1 || (de < 0 && pts < CERT_DIRECT_PTS)) && !ring_only) {
         const int nA = (a.j1 - a.j0 + 3) / 4, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + 3) / 4 : 0;
         if (nA + nB == 0) {
             *nblk = 0;
@@ -1110,12 +1065,9 @@ int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s) {
 
 // Float32 default: the pair kernel over whole chip-fulls of 512-point strips (as above);
 // QG_TEND_PAIR=0 selects the one-point kernel instead.
-#ifndef QG_PAIR_PF
-#define QG_PAIR_PF 1
-#endif
 template <int TX, class T>
 static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
-    constexpr int W = 2 * TX, PF = QG_PAIR_PF;
+    constexpr int W = 2 * TX, PF = 1;
     static int sl = 0;
     if (sl == 0) {
         int dev = 0, cus = 0, per = 0;
@@ -1213,7 +1165,7 @@ static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
     if (tend_variant() == 0 && tw == 0) {
         const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
         const int de = tend_direct_env();
-        if (de == 1 || (de < 0 && pts < QG_TEND_DIRECT_PTS)) return launch_tend_direct(a, s);
+        if (de == 1 || (de < 0 && pts < TEND_DIRECT_PTS)) return launch_tend_direct(a, s);
         // ~870^2 .. ~1750^2 points: 128-wide strips of 8 rows (tile sweep: 1024^2 35 vs 38 us)
         if (pts >= 0.75e6 && pts < 3.0e6) return launch_tend_variant<128, 1, T>(a, 8, s);
     }
