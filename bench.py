@@ -3,6 +3,10 @@ MI355X, with the HBM roofline of the dominant kernel and the CPU oracle timed be
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--n 4096] [--dt 60]
 
+N > 1 runs one process per GPU: under torch.distributed.run (RANK / WORLD_SIZE from the
+environment), or, launched plainly with WORLD_SIZE unset, bench.py starts the N rank
+processes itself (spawn_ranks; the parent never touches the GPU) and passes rank 0's line on.
+
 Workload (BASELINE.json configs[2]; per GPU for N > 1, slabs in y, weak scaling):
   2-layer Phillips, N x N interior per GPU, Float64, bench parameters of
   src/benchmarking/julia_bench_parts.jl:6-18 (H1 = 1 km, H2 = 2 km, beta = 2e-11,
@@ -236,8 +240,62 @@ def validate_record(out):
     return True
 
 
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_ranks(n, argv, cmd=None, timeout_s=None):
+    """Start n rank processes of `cmd` (default: this script with `argv`) with the
+    environment torch.distributed.run would give them (RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR = 127.0.0.1, a free MASTER_PORT), their stdout and stderr
+    passed through; wait for all of them.  If one fails, the others are stopped (they would
+    wait in a collective for it).  Returns the first failing exit code, else 0.  The parent
+    only starts processes: it never initialises the GPU."""
+    import signal
+    import subprocess
+
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + list(argv)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env))
+    rc = 0
+    t0 = time.monotonic()
+    live = list(procs)
+    while live:
+        time.sleep(0.05)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:  # (these exact children, nothing else)
+                    q.send_signal(signal.SIGTERM)
+        if timeout_s is not None and live and time.monotonic() - t0 > timeout_s:
+            rc = rc or 124
+            for q in live:
+                q.send_signal(signal.SIGTERM)
+            timeout_s = None
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     if args.graph:
         os.environ["QG_GRAPH"] = "1"
     import torch
@@ -246,8 +304,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
     torch.cuda.set_device(local if args.transport == "rccl" else local % max(1, torch.cuda.device_count()))
     dist = None
     if world > 1:

@@ -129,7 +129,9 @@ void qg_default_params(qg_params *p);
 int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out);
 int qg_destroy(qg_ctx *ctx);
 /* zeta, psi, f_store: device (M+2, P+2, 2, 3) arrays owned by the caller, of the element
- * type params.dtype names (double for QG_F64, float for QG_F32) */
+ * type params.dtype names (double for QG_F64, float for QG_F32), each 16-byte aligned
+ * (the slot moves run on 16-byte vectors; QG_ERR_INVALID_ARG otherwise -- every device
+ * allocator's base pointers are, only a sub-allocation at an odd offset is not) */
 int qg_bind_state(qg_ctx *ctx, void *zeta, void *psi, void *f_store);
 /* initialise_model (model.jl:37-62) on the device, seeded: psi_l interior (i, j) =
  * kick*U*Ly*u01(seed_l, i + M*j_global); zeroes all other slots and f_store; resets the

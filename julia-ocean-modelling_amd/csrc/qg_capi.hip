@@ -276,6 +276,8 @@ static int settle_pcg(qg_ctx *c) {
 // (the arrays bound before must still be valid here: a pending certification reads them)
 int qg_bind_state(qg_ctx *c, void *zeta, void *psi, void *f_store) {
     if (!c || !zeta || !psi || !f_store) return QG_ERR_INVALID_ARG;
+    for (const void *b : {zeta, psi, f_store})  // (launch_slot_move's 16-byte vectors)
+        if (reinterpret_cast<uintptr_t>(b) % 16 != 0) return QG_ERR_INVALID_ARG;
     if (c->zeta) QG_CHECK(settle_pcg(c));
     drop_graphs(c);
     c->zeta = zeta;
@@ -421,7 +423,7 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
             if (c->pcg && c->pcg->pending()) {
                 c->pcg->fill_cert_args(a);
                 int nblk = 0;
-                QG_CHECK(launch_tendency_cert(a, &nblk, c->stream));
+                QG_CHECK(launch_tendency_cert(a, c->pcg->cert_capacity(), &nblk, c->stream));
                 QG_CHECK(c->pcg->latch_fused(nblk, c->stream));
                 done = true;
             }
@@ -459,7 +461,7 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
             in.j0 = 2;
             in.j1 = (int)p.P - 2;
             in.j2 = in.j3 = 0;
-            QG_CHECK(launch_tendency(in, c->stream));
+            QG_CHECK(launch_tendency(in, c->stream, true));
             QG_HIP(hipStreamWaitEvent(c->stream, c->ov_halo, 0));
             TendArgsT<T> bd = a;  // rows 0, 1 and P-2, P-1: one launch, two row ranges
             bd.j0 = 0;
@@ -488,11 +490,17 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
 }
 
 // Deferred PCG: report new certification failures the device has latched.  Non-blocking
-// (wait = false): every QG_PACE_STEPS steps, read the copy of the latch made one interval
-// earlier if it has landed, then start a new copy.  Blocking (wait = true, the end of qg_run):
-// settle the pending check and read the latch now.
-static int poll_pcg(qg_ctx *c, bool wait) {
+// (wait = false, `steps` more steps enqueued on stream `on`): every QG_PACE_STEPS steps, read
+// the copy of the latch made one interval earlier, then start a new copy.  On one rank that
+// read is skipped while the copy is still in flight.  With a transport every rank reads it
+// (a bounded wait; the copy is an interval old and has normally landed): the verdict comes
+// from all-gathered sums and is the same on every rank, so all ranks stop at the same step --
+// one rank returning while its peers step into the next exchange would leave them in a
+// mismatched collective.  Blocking (wait = true, the end of qg_run): settle the pending check
+// and read the latch now.
+static int poll_pcg(qg_ctx *c, bool wait, int steps = 1, hipStream_t on = nullptr) {
     if (!c->pcg || !c->pcg->deferred() || c->capturing) return QG_OK;
+    if (!on) on = c->stream;
     if (!c->latch_host) {
         QG_HIP(hipHostMalloc((void **)&c->latch_host, sizeof(double) * 8, hipHostMallocDefault));
         QG_HIP(hipEventCreateWithFlags(&c->latch_ev, hipEventDisableTiming));
@@ -515,16 +523,22 @@ static int poll_pcg(qg_ctx *c, bool wait) {
         c->latch_armed = false;
         return report();
     }
-    if (++c->poll_count % QG_PACE_STEPS != 0) return QG_OK;
+    const int64_t before = c->poll_count;
+    c->poll_count += steps;
+    if (before / QG_PACE_STEPS == c->poll_count / QG_PACE_STEPS) return QG_OK;
     if (c->latch_armed) {
-        const hipError_t q = hipEventQuery(c->latch_ev);
-        if (q == hipErrorNotReady) return QG_OK;  // the last copy is still in flight
-        QG_HIP(q);
+        if (c->distributed) {
+            QG_CHECK(comm_wait(c->comm, on, c->latch_ev, "qg_evolve_psi (PCG latch)"));
+        } else {
+            const hipError_t q = hipEventQuery(c->latch_ev);
+            if (q == hipErrorNotReady) return QG_OK;  // the last copy is still in flight
+            QG_HIP(q);
+        }
         c->latch_armed = false;
         QG_CHECK(report());
     }
-    QG_HIP(hipMemcpyAsync(c->latch_host, c->pcg->latch(), sizeof(double) * 8, hipMemcpyDeviceToHost, c->stream));
-    QG_HIP(hipEventRecord(c->latch_ev, c->stream));
+    QG_HIP(hipMemcpyAsync(c->latch_host, c->pcg->latch(), sizeof(double) * 8, hipMemcpyDeviceToHost, on));
+    QG_HIP(hipEventRecord(c->latch_ev, on));
     c->latch_armed = true;
     return QG_OK;
 }
@@ -648,10 +662,18 @@ int qg_run(qg_ctx *c, int64_t first_step, int64_t nsteps) {
             const int64_t cycles = (end - t) / 3;
             QG_HIP(hipEventRecord(c->gev_in, c->stream));  // after the caller's earlier work
             QG_HIP(hipStreamWaitEvent(c->gstream, c->gev_in, 0));
-            for (int64_t k = 0; k < cycles; ++k) QG_HIP(hipGraphLaunch(g, c->gstream));
+            int st = QG_OK;
+            int64_t k = 0;
+            while (k < cycles && st == QG_OK) {
+                QG_HIP(hipGraphLaunch(g, c->gstream));
+                ++k;
+                // deferred PCG: the bounded-delay latch poll between replays, as qg_step does it
+                if (c->pcg) st = poll_pcg(c, false, 3, c->gstream);
+            }
             QG_HIP(hipEventRecord(c->gev_out, c->gstream));
             QG_HIP(hipStreamWaitEvent(c->stream, c->gev_out, 0));  // before the caller's later work
-            t += 3 * cycles;
+            t += 3 * k;
+            if (st != QG_OK) return st;
         }
     }
     for (; t < end; ++t) QG_CHECK(qg_step(c, t));

@@ -202,11 +202,14 @@ inline double wind_row(double tau0, double rho0, double H1, double dx, int64_t P
     return -A * std::sin(pi2 * (((double)jg + 0.5) / (double)P_total));
 }
 
-int launch_tendency(const TendArgsT<double> &a, hipStream_t s);
-int launch_tendency(const TendArgsT<float> &a, hipStream_t s);
+// room = true: every CU keeps OVERLAP_LDS_ROOM bytes of LDS free while this launch runs (the
+// halo overlap's interior rows: the exchange kernel on the side stream needs a slot beside them)
+int launch_tendency(const TendArgsT<double> &a, hipStream_t s, bool room = false);
+int launch_tendency(const TendArgsT<float> &a, hipStream_t s, bool room = false);
 // the same tendency, both layers per workgroup, also certifying the previous solve (a.cert):
-// *nblk = workgroups launched (partials written)
-int launch_tendency_cert(const TendArgsT<double> &a, int *nblk, hipStream_t s);
+// *nblk = workgroups launched (partials written); a grid of more than `cap` workgroups (the
+// partials' capacity) is refused before anything is launched
+int launch_tendency_cert(const TendArgsT<double> &a, int64_t cap, int *nblk, hipStream_t s);
 int launch_laplace(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
 int launch_cd(const double *u, double *out, int64_t M, int64_t P, double dx, hipStream_t s);
 int launch_arakawa(const double *z, const double *p, double *out, int64_t M, int64_t P, double dx,

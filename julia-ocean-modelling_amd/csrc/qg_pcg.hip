@@ -468,8 +468,9 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
     const size_t F = (size_t)(M + 2) * (size_t)(P + 2);
     nblk_ = (int)(((M + PCG_T - 1) / PCG_T) * std::min<int64_t>(P, PCG_ROWB));
     // certifying tendency: at most one workgroup per 64 columns and 4 rows (the widest
-    // partial grid: the cache-resident form's 64 x 4 blocks; the ring form uses fewer)
-    cert_part_n_ = ((M + 63) / 64) * std::max<int64_t>(1, (P + 3) / 4);
+    // partial grid: the cache-resident form's 64 x 4 blocks; the ring form uses fewer), plus
+    // one block row for a launch split over two row ranges
+    cert_part_n_ = ((M + 63) / 64) * (std::max<int64_t>(1, (P + 3) / 4) + 1);
     const size_t bytes = sizeof(double) * (10 * F + 6 * (size_t)nblk_ + 64 + 6 * (size_t)nranks + 8 +
                                            4 * (size_t)cert_part_n_);
     if (hipMalloc(&mem_, bytes) != hipSuccess) {

@@ -52,6 +52,8 @@ public:
     void fill_cert_args(TendArgsT<double> &t) const;
     // after launch_tendency_cert: fold its nblk partials and latch the verdict
     int latch_fused(int nblk, hipStream_t s);
+    // workgroups a certifying tendency may write partials for (launch_tendency_cert's cap)
+    int64_t cert_capacity() const { return cert_part_n_; }
     // a pending fused certification with no tendency coming: run the check pass now
     int certify_pending(hipStream_t s, SpectralSolver::GatherFn gather = nullptr, void *user = nullptr);
     // latch record (device, doubles): [0] solves certified, [1] failures, [2] first failing

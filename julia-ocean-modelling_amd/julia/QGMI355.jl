@@ -174,17 +174,26 @@ end
 
 """`unbind!(zeta, psi, f_store)` / `unbind!()`: release the cached context of the
 reference-signature calls bound to these arrays (or all of them); the cache holds the arrays,
-so without this they stay alive.  Returns the number released."""
+so without this they stay alive.  Returns the number released.  Every selected context is
+released even if settling one throws (a failed deferred PCG certificate); the first error is
+rethrown after all of them are released."""
 function unbind!(zeta=nothing, psi=nothing, f_store=nothing)
     keys_ = zeta === nothing ? collect(keys(_BOUND)) :
             [k for k in keys(_BOUND) if k[1] == UInt(pointer(zeta)) &&
              (psi === nothing || k[2] == UInt(pointer(psi))) &&
              (f_store === nothing || k[3] == UInt(pointer(f_store)))]
+    err = nothing  # every context is released; the first failure is thrown after
     for k in keys_
         s = pop!(_BOUND, k)
-        @qgcheck qg_synchronize ccall((:qg_synchronize, libqg), Cint, (Ptr{Cvoid},), s.ctx)
-        finalize(s)
+        try
+            @qgcheck qg_synchronize ccall((:qg_synchronize, libqg), Cint, (Ptr{Cvoid},), s.ctx)
+        catch e
+            err === nothing && (err = e)
+        finally
+            finalize(s)
+        end
     end
+    err === nothing || throw(err)
     length(keys_)
 end
 

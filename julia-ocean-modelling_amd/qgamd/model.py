@@ -231,11 +231,15 @@ class State:
         self.rank, self.nranks = rank, nranks
         self._attached_ranks = 1
 
-    def __del__(self):
+    def close(self):
+        """Destroy the library context now (qg_destroy); the arrays stay with the caller."""
         ctx = getattr(self, "_ctx", None)
         if ctx and _lib._lib is not None:
             _lib._lib.qg_destroy(ctx)
             self._ctx = None
+
+    def __del__(self):
+        self.close()
 
     # -- multi-GPU ---------------------------------------------------------------------
     def comm_init(self, nranks, rank, uid: bytes):
@@ -372,8 +376,9 @@ def _bound_state(m, zeta, psi, f_store):
     key = (zeta.data_ptr(), psi.data_ptr(), f_store.data_ptr())
     st = _BOUND.get(key)
     if st is None or st.model != m:
-        if st is not None:
-            st.synchronize()  # settle the old context's pending work on these arrays
+        if st is not None:  # settle and release the old context (its failure is raised after)
+            st = None
+            unbind(zeta, psi, f_store)
         st = _BOUND[key] = State(m, device=zeta.device, dtype=zeta.dtype, arrays=(zeta, psi, f_store))
         st.set_keep_order(True)
     return st
@@ -382,17 +387,27 @@ def _bound_state(m, zeta, psi, f_store):
 def unbind(zeta=None, psi=None, f_store=None):
     """Release the cached contexts of the reference-signature calls: the one bound to these
     arrays, or all of them (no arguments).  The contexts hold references to the arrays, so
-    without this the arrays stay alive as long as the process."""
+    without this the arrays stay alive as long as the process.  Every selected context is
+    released even if settling one fails (e.g. a deferred PCG certificate that failed,
+    QG_ERR_NOT_CONVERGED); the first such error is raised after all of them are released."""
     if zeta is None:
         keys = list(_BOUND)
     else:
         keys = [k for k in _BOUND if k[0] == zeta.data_ptr()
                 and (psi is None or k[1] == psi.data_ptr())
                 and (f_store is None or k[2] == f_store.data_ptr())]
+    err = None
     for k in keys:
         st = _BOUND.pop(k)
-        st.synchronize()
-        del st
+        try:
+            st.synchronize()
+        except Exception as e:  # noqa: BLE001 -- re-raised below, after every release
+            err = err or e
+        finally:
+            st.close()
+            del st
+    if err is not None:
+        raise err
     return len(keys)
 
 

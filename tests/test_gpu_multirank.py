@@ -163,3 +163,78 @@ def test_keep_order_slabs_bit_identical(world, M, P, steps, solver):
     for r in range(world):
         for n in ("zeta", "psi", "f_store", "diag"):
             assert np.array_equal(base[r][n], keep[r][n]), (r, n)
+
+
+def _cert_fail_worker(rank, world, port, M, P, outdir):
+    import sys
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import qgamd
+    from qgamd.hostcomm import TorchDistTransport
+
+    m = qgamd.bench_model(M, P=P)
+    res = {}
+    # the reference's loop, one call per step: every rank must stop at the same step
+    st = qgamd.State(m, P_local=P // world, solver=1, pcg_rtol=1e-30)
+    TorchDistTransport().attach(st, world, rank)
+    st.initialise()
+    res["stop"] = -1
+    for t in range(1, 200):
+        st.evolve_zeta_(t)
+        try:
+            st.evolve_psi_()
+        except qgamd.QGError as e:
+            res["status"] = e.status
+            res["stop"] = t
+            break
+    res["cert"] = st.pcg_certificate()
+    # qg_run: the same stop on every rank
+    st2 = qgamd.State(m, P_local=P // world, solver=1, pcg_rtol=1e-30)
+    TorchDistTransport().attach(st2, world, rank)
+    st2.initialise()
+    try:
+        st2.run(1, 300)
+        res["run_status"] = 0
+    except qgamd.QGError as e:
+        res["run_status"] = e.status
+    res["run_cert"] = st2.pcg_certificate()
+    import json
+    open(os.path.join(outdir, f"cert{rank}.json"), "w").write(json.dumps(res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_failed_certificate_stops_every_rank_at_the_same_step(world):
+    """Deferred PCG with an unreachable residual target across slabs (host transport): the
+    latch poll is collective, so every rank reports QG_ERR_NOT_CONVERGED (-7) at the same step
+    and none steps on into an exchange its peers never post."""
+    import json
+
+    import torch
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_cert_fail_worker, args=(r, world, port, 64, 64, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=300)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        res = [json.load(open(os.path.join(d, f"cert{r}.json"))) for r in range(world)]
+    assert all(r["status"] == -7 for r in res), res
+    assert len({r["stop"] for r in res}) == 1 and 16 <= res[0]["stop"] <= 3 * 16 + 1, res
+    assert len({json.dumps(r["cert"], sort_keys=True) for r in res}) == 1, res
+    assert all(r["run_status"] == -7 for r in res), res
+    assert len({r["run_cert"]["solves"] for r in res}) == 1 and res[0]["run_cert"]["solves"] < 300, res

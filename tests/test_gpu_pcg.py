@@ -122,6 +122,14 @@ def test_deferred_certificate_fused_in_tendency(env, N, steps):
     # the host-checked form's stand-alone pass: the same residual, at roundoff too
     sb = b.stats()
     assert sb["iters"] == [1, 1] and max(sb["relres"]) < 1e-13, sb
+    # and the PCG trajectory itself against the C oracle (BASELINE config 2 at 1024^2: the
+    # Arakawa tendency + Helmholtz PCG per step), psi and zeta at the north-star bar
+    ref = O.State(R.bench_model(N)).run(steps)
+    for n in ("psi", "zeta"):
+        want, got = getattr(ref, n)[:, :, :, 0], a.to_numpy(n)[:, :, :, 0]
+        e = np.linalg.norm(got - want) / np.linalg.norm(want)
+        print(f"deferred PCG {N}^2 x {steps} steps vs C oracle, {n}: {e:.3e}")
+        assert e < 1e-10, (n, e)
 
 
 def test_deferred_certificate_failure_is_reported(env):
@@ -180,6 +188,19 @@ def test_deferred_pcg_graph_replay(env, monkeypatch):
         assert np.array_equal(a.to_numpy(n), b.to_numpy(n)), n
     c = b.pcg_certificate()
     assert c["solves"] == 14 and c["failures"] == 0, c
+
+
+def test_deferred_failure_stops_graph_replay(env, monkeypatch):
+    """QG_GRAPH=1: the replayed step graphs are polled between replays like stream steps, so a
+    failed certificate stops a long run within a few polling intervals."""
+    torch, qg, R, O = env
+    monkeypatch.setenv("QG_GRAPH", "1")
+    st = qg.initialise_model(qg.bench_model(64), solver=1, pcg_rtol=1e-30)
+    with pytest.raises(qg.QGError) as e:
+        st.run(1, 600)
+    assert e.value.status == -7
+    c = st.pcg_certificate()
+    assert 16 <= c["solves"] <= 3 * 16 + 4 and c["failures"] == c["solves"], c
 
 
 def test_plain_cg_256(env):
