@@ -18,7 +18,7 @@ for k in 1 2 3; do
 done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/$O/trace -o ov -- python3 $R/bench.py --comm-self --overlap --steps 30 --warmup 10 --pcg-steps 0 --dropin-steps 0 --cpu-steps 0 --comm-probe-reps 0 > $R/$O/trace.log 2>&1 || exit 4
-python3 $R/tools/timeline.py $R/$O/trace/ov_kernel_trace.csv tendency_kernel 3 > $R/$O/timeline.txt
+python3 $R/tools/timeline.py $R/$O/trace/ov_kernel_trace.csv spec_carry 3 > $R/$O/timeline.txt
 head -30 $R/$O/timeline.txt
 cd $R
 timeout -k 10 300 python tools/cg_floor.py 256 > $O/cg_floor.txt 2>&1
