@@ -164,7 +164,8 @@ int qg_get_stats(qg_ctx *ctx, qg_stats *out);
  * its verdict is latched there: no host round trip, qg_run can replay PCG steps as HIP graphs.
  * A failed certification is reported (QG_ERR_NOT_CONVERGED, once) by qg_evolve_psi / qg_step
  * within two polling intervals (the latch is copied to the host every QG_PACE_STEPS solves and
- * read one interval later, without blocking), by the end of qg_run (it settles and reads the
+ * read one interval later, waiting for that copy if needed: the host stays at most two
+ * intervals ahead, so every rank stops at the same step, graph replays included), by the end of qg_run (it settles and reads the
  * latch), by qg_synchronize, and in qg_pcg_certificate's record.  sync = 1 (or QG_PCG_SYNC=1 at create): the host reads every
  * residual and runs the general PCG iteration when the certificate fails (the old form).  */
 int qg_set_pcg_sync(qg_ctx *ctx, int sync);

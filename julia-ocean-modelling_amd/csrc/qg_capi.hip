@@ -489,15 +489,15 @@ int qg_evolve_zeta(qg_ctx *c, int64_t timestep) {
     return c->esize == sizeof(float) ? evolve_zeta_t<float>(c, timestep) : evolve_zeta_t<double>(c, timestep);
 }
 
-// Deferred PCG: report new certification failures the device has latched.  Non-blocking
-// (wait = false, `steps` more steps enqueued on stream `on`): every QG_PACE_STEPS steps, read
-// the copy of the latch made one interval earlier, then start a new copy.  On one rank that
-// read is skipped while the copy is still in flight.  With a transport every rank reads it
-// (a bounded wait; the copy is an interval old and has normally landed): the verdict comes
-// from all-gathered sums and is the same on every rank, so all ranks stop at the same step --
-// one rank returning while its peers step into the next exchange would leave them in a
-// mismatched collective.  Blocking (wait = true, the end of qg_run): settle the pending check
-// and read the latch now.
+// Deferred PCG: report new certification failures the device has latched.  Polling (wait =
+// false, `steps` more steps enqueued on stream `on`): every QG_PACE_STEPS steps, read the copy
+// of the latch made one interval earlier -- waiting for it if it has not landed (bounded), so
+// the host is never more than two intervals ahead of the device and a failure is reported at
+// a fixed step count: on one rank whatever the host's lead (graph replays enqueue far faster
+// than the device runs them), and with a transport at the same step on every rank (the verdict
+// comes from all-gathered sums, identical everywhere; one rank returning while its peers step
+// into the next exchange would leave them in a mismatched collective).  Final (wait = true,
+// the end of qg_run): settle the pending check and read the latch now.
 static int poll_pcg(qg_ctx *c, bool wait, int steps = 1, hipStream_t on = nullptr) {
     if (!c->pcg || !c->pcg->deferred() || c->capturing) return QG_OK;
     if (!on) on = c->stream;
@@ -527,13 +527,7 @@ static int poll_pcg(qg_ctx *c, bool wait, int steps = 1, hipStream_t on = nullpt
     c->poll_count += steps;
     if (before / QG_PACE_STEPS == c->poll_count / QG_PACE_STEPS) return QG_OK;
     if (c->latch_armed) {
-        if (c->distributed) {
-            QG_CHECK(comm_wait(c->comm, on, c->latch_ev, "qg_evolve_psi (PCG latch)"));
-        } else {
-            const hipError_t q = hipEventQuery(c->latch_ev);
-            if (q == hipErrorNotReady) return QG_OK;  // the last copy is still in flight
-            QG_HIP(q);
-        }
+        QG_CHECK(comm_wait(c->distributed ? c->comm : nullptr, on, c->latch_ev, "qg_evolve_psi (PCG latch)"));
         c->latch_armed = false;
         QG_CHECK(report());
     }

@@ -16,9 +16,13 @@
 // complex multiply to combine).
 //
 // LDS layouts: a pass with stride NS < 8 scatters with a lane stride of NS*16 B, which
-// conflicts in the 8-lane groups of ds_write_b128; its output buffer uses lpad (one pad slot
-// per 8 values).  All other buffers (caller-written rows, wide-stride pass outputs) are read
-// and written contiguously and use the identity layout.
+// conflicts in the 8-lane groups of ds_write_b128; its output buffer is XOR-swizzled within
+// aligned 8-element blocks, x ^ ((x >> 3) & 7).  That is conflict-free both for those writes
+// and for the next pass's contiguous ds_read_b128 (16-lane groups, 64 banks); a pad slot per 8
+// values (the layout before) fixed the writes but left those reads 2-way conflicted: 256
+// extra LDS cycles per 4096-point row, measured as SQ_LDS_BANK_CONFLICT in the wide-row passes
+// (tools/lds_bank_model.py models both).  All other buffers (caller-written rows, wide-stride
+// pass outputs) are read and written contiguously and use the identity layout.
 #pragma once
 
 #include "qg_common.hpp"
@@ -88,11 +92,11 @@ struct PassRadix {
 __host__ __device__ constexpr int lpad(int x) { return x + (x >> 3); }
 template <int NS>  // layout of the buffer written by the pass with stride NS (caller: NS = 0)
 __device__ __forceinline__ int lay(int x) {
-    if constexpr (NS > 0 && NS < 8) return lpad(x);
+    if constexpr (NS > 0 && NS < 8) return x ^ ((x >> 3) & 7);
     else return x;
 }
 template <int N>
-struct LdsSize {  // complex elements of one row buffer (any layout)
+struct LdsSize {  // complex elements of one row buffer (any layout; sized for the padded one)
     static constexpr int value = lpad(N - 1) + 1;
 };
 

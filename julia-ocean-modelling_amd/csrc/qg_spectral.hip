@@ -1035,14 +1035,13 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     using PV = typename Pair<S>::V;
     // half_tmp holds psi~1 in the state's precision (like u: F32 intermediates for F32 states)
     typedef S PD __attribute__((ext_vector_type(2)));  // half_tmp pair (aligned: rows of M)
-    using Inv = FftFromReg<HN, HT, true>;
     constexpr int s = SYS;
     extern __shared__ double2 lds[];
     double2 *b0 = lds, *b1 = lds + LdsSize<HN>::value, *twl = lds + 2 * LdsSize<HN>::value;
     double2 *wlo = twl + HPlan::TW, *whi = wlo + 64;
     // the split step exchanges X through b1: the first inverse pass writes only b0
     double2 *Xs = b1;
-    const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
+    static_assert(HPlan::REG_OUT && HPlan::NPASS == 4, "last pass to registers, reading b0");
     half_lds_init(a, twl, wlo, whi);
     const int t = threadIdx.x, c = blockIdx.x;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
@@ -1158,22 +1157,22 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                 in[q] = make_double2(A.x - B.y, A.y + B.x);
             }
         }
-        // first inverse pass, then the next row's loads (in[] dead), then the remaining passes
+        // first inverse pass, then the next row's loads (in[] dead), then the remaining passes;
+        // the last pass leaves its output in registers (element t + p HT: the row order of the
+        // stores below), so a row writes the LDS four times (split step + three passes), not five
         const int tt = opaque_tid();
         fft_pass<HN, HT, 1, 0, true, true, false>(nullptr, b0, twl, tt, in);
         if (j < e) load_u(j + 1);
         if constexpr (SYS == 1) load_y(j);
-        {
-            double2 dummy[HPlan::R_LAST];
-            fft_run<HN, HT, HPlan::R0, 1, true, false>(b0, b1, twl, tt, dummy);
-        }
+        double2 xo[HPlan::R_LAST];
+        fft_run<HN, HT, HPlan::R0, 1, true, true>(b0, b1, twl, tt, xo);
         if constexpr (SYS == 0) {
             S *yr = static_cast<S *>(a.half_tmp) + (size_t)j * a.M;
             const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
 #pragma unroll
             for (int p = 0; p < HK; ++p) {
                 const int n = t + p * HT;
-                const double2 z = Xb[lay<HPlan::LAST_NS>(n)];
+                const double2 z = xo[p];
                 PD v;
                 // the pinned unknown is exactly 0 (get_poisson_cholesky's identity row)
                 v.x = (S)((pin_row && n == 0) ? 0.0 : z.x - pin);
@@ -1200,7 +1199,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 #pragma unroll
             for (int p = 0; p < HK; ++p) {
                 const int n = t + p * HT;
-                const double2 z = Xb[lay<HPlan::LAST_NS>(n)];
+                const double2 z = xo[p];
                 const double x1a = (double)y1[p].x, x1b = (double)y1[p].y;
                 PV v1;
                 v1.x = (S)(a.pin_out[0] * x1a + a.pin_out[1] * z.x);
@@ -1218,7 +1217,9 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
             asm volatile("" ::: "memory");
             if (j < e) load_coef();
         }
-        __syncthreads();  // the next row's split step writes Xs = b1 (which holds this result)
+        // (no barrier: the last pass read b0, and the next row's first write of b0 follows the
+        // split step's barrier; b1, which the next split step writes, was last read by the
+        // third pass, before its own barrier)
     }
 }
 

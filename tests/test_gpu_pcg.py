@@ -155,7 +155,7 @@ def test_deferred_certificate_failure_is_reported(env):
     assert e.value.status == -7
     st2.synchronize()
     assert st2.pcg_certificate()["failures"] == 5
-    # a long run stops early (the non-blocking latch poll every 16 steps)
+    # a long run stops early (the latch poll every 16 steps reads the copy of the interval before)
     st3 = qg.initialise_model(qg.bench_model(64), solver=1, pcg_rtol=1e-30)
     with pytest.raises(qg.QGError) as e:
         st3.run(1, 400)
