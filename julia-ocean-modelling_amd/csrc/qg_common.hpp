@@ -86,9 +86,14 @@ __device__ __forceinline__ void store_with_ghosts(T *out, int64_t ld, int64_t M,
 // Same as store_with_ghosts for a whole row j that the caller walks: `row` = out + (j+1)*ld
 // and the ghost-row target `grow` (row 0 when j == P-1, row P+1 when j == 0, else nullptr)
 // are wave-uniform, so every store is an SGPR base + 32-bit lane offset.
-template <class T>
+// EDGE = false: i is neither column 0 nor M-1 (a strip away from the row ends)
+template <class T, bool EDGE = true>
 __device__ __forceinline__ void store_row_with_ghosts(T *row, T *grow, int M, int i, T v) {
     st_stream(row + i + 1, v);
+    if constexpr (!EDGE) {
+        if (grow) grow[i + 1] = v;
+        return;
+    }
     if (i == M - 1) row[0] = v;
     if (i == 0) row[M + 1] = v;
     if (grow) {

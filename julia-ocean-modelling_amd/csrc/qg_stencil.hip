@@ -116,42 +116,16 @@ __device__ __forceinline__ TendBlock tend_block() {
 // per point and system, b_s = -(proj_in zeta)_s and r_s = b_s + (A_s psi~)_s with psi~ =
 // P_fwd^-1 psi, A_s psi~ = sum_l P_fwd^-1[s][l] (lap(psi_l) + alpha_s psi_l) (lap(psi_l) is
 // the ring's own), summed over the two layers through LDS; (b,b), (r,r) per workgroup.
-template <int TX, int PF, class T, bool CERT = false>
-__global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
+// One strip (see tendency_pair_strip for EDGE: false = the x-halo inside the row, so no
+// periodic wraps and no ghost-column stores in the row loop).
+template <int TX, int PF, class T, bool CERT, bool EDGE>
+__device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer, int t, int x0, int jb0, int jb1,
+                                               T (*sp)[TX + 4], T (*sz)[TX + 2], T (*sl)[TX + 2],
+                                               double (*xch)[4][CERT ? TX : 1]) {
     constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
-    constexpr int NL = CERT ? 2 : 1;       // layers per workgroup
-    const TendBlock tb = tend_block();
-    // (wave-uniform: TX is a whole number of waves; in an SGPR the per-layer pointers stay
-    // scalar loads -- a per-lane index made them vector loads, re-issued every row)
-    const int layer = CERT ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x / TX)) : tb.z;
-    const int t = CERT ? (int)(threadIdx.x % TX) : (int)threadIdx.x;
     const int M = (int)a.M, P = (int)a.P;
     const int64_t ld = a.ld;
-    const int x0 = tb.x * TX;
     const int i = x0 + t;
-    // strip rows: range A = [j0, j1) split evenly over nyA workgroups along y, then range B
-    const int y = tb.y;
-    const bool second = y >= nyA;
-    const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
-    const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
-    const int jb0 = r0 + (int)(((int64_t)yy * nr) / ny);
-    const int jb1 = r0 + (int)(((int64_t)(yy + 1) * nr) / ny);
-    if (jb0 >= jb1) {  // uniform over the block
-        if constexpr (CERT) {
-            if (threadIdx.x < 4) a.cert[4 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = 0;
-        }
-        return;
-    }
-
-    __shared__ T sp_[NL][RP][TX + 4];
-    __shared__ T sz_[NL][RZ][TX + 2];
-    __shared__ T sl_[NL][RL][TX + 2];
-    T(&sp)[RP][TX + 4] = sp_[CERT ? layer : 0];
-    T(&sz)[RZ][TX + 2] = sz_[CERT ? layer : 0];
-    T(&sl)[RL][TX + 2] = sl_[CERT ? layer : 0];
-    // CERT: layer 1's (b0, r0, b1, r1) contributions of row j, read by layer 0 after the next
-    // barrier (double-buffered by row parity); layer 0 keeps its own for that row meanwhile
-    __shared__ double xch[CERT ? 2 : 1][4][CERT ? TX : 1];
     double cv[4] = {0, 0, 0, 0};  // (b0,b0), (r0,r0), (b1,b1), (r1,r1)
     double pend[4] = {0, 0, 0, 0};
     int pend_j = -1;
@@ -185,6 +159,7 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
     const bool small = M < TX + 4;
 
     auto wx = [&](int x) -> int {  // periodic wrap of an interior column index
+        if constexpr (!EDGE) return x;
         if (small) return ((x % M) + M) % M;
         return x < 0 ? x + M : (x >= M ? x - M : x);
     };
@@ -198,7 +173,7 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
     const int xo = wx(i);
     const int xph = ph_q >= 0 ? wx(x0 - 2 + ph_q) : 0;
     const int xzh = zh_q >= 0 ? wx(x0 - 1 + zh_q) : 0;
-    const bool has_out = i < M;
+    const bool has_out = !EDGE || i < M;
     const bool ab3 = a.ab3 != 0;
 
     // prefetch pipeline PF rows deep: slot 0 is consumed next
@@ -340,12 +315,12 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
                              : zcen + (dtT * F);
             T *zo = a.zeta_out[layer], *fo = a.f_out[layer];
             const bool gr = a.write_ghost_rows;
-            store_row_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
-            store_row_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
+            store_row_with_ghosts<T, EDGE>(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
+            store_row_with_ghosts<T, EDGE>(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
             if (ab3 && a.fshift1[layer]) {  // (see TendArgsT::fshift1)
                 T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
-                store_row_with_ghosts(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, i, f1c);
-                store_row_with_ghosts(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, i, f2c);
+                store_row_with_ghosts<T, EDGE>(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, i, f1c);
+                store_row_with_ghosts<T, EDGE>(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, i, f2c);
             }
             if constexpr (CERT) {  // this layer's parts of b_s and r_s at (i, j)
                 double part[4];
@@ -388,6 +363,43 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
     }
 }
 
+template <int TX, int PF, class T, bool CERT = false>
+__global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
+    constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
+    constexpr int NL = CERT ? 2 : 1;       // layers per workgroup
+    const TendBlock tb = tend_block();
+    // (wave-uniform: TX is a whole number of waves; in an SGPR the per-layer pointers stay
+    // scalar loads -- a per-lane index made them vector loads, re-issued every row)
+    const int layer = CERT ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x / TX)) : tb.z;
+    const int t = CERT ? (int)(threadIdx.x % TX) : (int)threadIdx.x;
+    const int M = (int)a.M;
+    const int x0 = tb.x * TX;
+    // strip rows: range A = [j0, j1) split evenly over nyA workgroups along y, then range B
+    const int y = tb.y;
+    const bool second = y >= nyA;
+    const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
+    const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
+    const int jb0 = r0 + (int)(((int64_t)yy * nr) / ny);
+    const int jb1 = r0 + (int)(((int64_t)(yy + 1) * nr) / ny);
+    if (jb0 >= jb1) {  // uniform over the block
+        if constexpr (CERT) {
+            if (threadIdx.x < 4) a.cert[4 * ((size_t)blockIdx.y * gridDim.x + blockIdx.x) + threadIdx.x] = 0;
+        }
+        return;
+    }
+    __shared__ T sp_[NL][RP][TX + 4];
+    __shared__ T sz_[NL][RZ][TX + 2];
+    __shared__ T sl_[NL][RL][TX + 2];
+    // CERT: layer 1's (b0, r0, b1, r1) contributions of row j, read by layer 0 after the next
+    // barrier (double-buffered by row parity); layer 0 keeps its own for that row meanwhile
+    __shared__ double xch[CERT ? 2 : 1][4][CERT ? TX : 1];
+    const int L = CERT ? layer : 0;
+    if (x0 >= 2 && x0 + TX + 2 <= M)  // (uniform) the x-halo inside the row
+        tendency_strip<TX, PF, T, CERT, false>(a, layer, t, x0, jb0, jb1, sp_[L], sz_[L], sl_[L], xch);
+    else
+        tendency_strip<TX, PF, T, CERT, true>(a, layer, t, x0, jb0, jb1, sp_[L], sz_[L], sl_[L], xch);
+}
+
 // ------------------------------------------------------------------------------------
 // Float32 tendency, two points per thread (register blocking).  With F32 fields the kernel
 // above moves half the bytes but keeps its per-point LDS reads and per-row barrier, and is
@@ -412,11 +424,16 @@ struct PairT<double> {
     typedef double VU __attribute__((ext_vector_type(2), aligned(8)));
 };
 
-// store the pair (xa, xa+1) of row j with its periodic images (store_row_with_ghosts x 2)
-template <class T>
+// store the pair (xa, xa+1) of row j with its periodic images (store_row_with_ghosts x 2);
+// EDGE = false: a pair of an interior strip (both points in range, neither column 0 nor M-1)
+template <class T, bool EDGE = true>
 __device__ __forceinline__ void store_pair_with_ghosts(T *row, T *grow, int M, int xa, T v0, T v1, bool has_b) {
     using VU = typename PairT<T>::VU;
     auto put = [&](T *r) {
+        if constexpr (!EDGE) {
+            *(VU *)(r + xa + 1) = VU{v0, v1};
+            return;
+        }
         if (has_b) {
             *(VU *)(r + xa + 1) = VU{v0, v1};
             if (xa + 1 == M - 1) r[0] = v1;
@@ -430,30 +447,20 @@ __device__ __forceinline__ void store_pair_with_ghosts(T *row, T *grow, int M, i
     if (grow) put(grow);
 }
 
-// PF: register prefetch depth in rows (as tendency_kernel's)
-template <int TX, class T, int PF = 1>
-__global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int nyA, int nyB) {
+// One strip of the pair kernel.  EDGE = false (every strip whose x-halo lies inside the row:
+// all but the first and the last): no periodic wrap of column indices, every pair in range,
+// no ghost-column stores -- the interior strips' row loop is straight-line code except for
+// the halo lanes.  EDGE = true: the general form (wraps, partial pairs, ghost columns).
+template <int TX, class T, int PF, bool EDGE>
+__device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int layer, int x0, int jb0, int jb1,
+                                                    T (*sp)[2 * TX + 4], T (*sz)[2 * TX + 4], T (*sl)[2 * TX + 4]) {
     using V = typename PairT<T>::V;
     using VU = typename PairT<T>::VU;
-    constexpr int RP = 6, RZ = 5, RL = 4, W = 2 * TX, WL = W + 4;
-    const TendBlock tb = tend_block();
-    const int layer = tb.z;
+    constexpr int RP = 6, RZ = 5, RL = 4, W = 2 * TX;
     const int t = threadIdx.x;
     const int M = (int)a.M, P = (int)a.P;
     const int64_t ld = a.ld;
-    const int x0 = tb.x * W;
     const int xa = x0 + 2 * t;  // own points xa, xa + 1
-    const int y = tb.y;
-    const bool second = y >= nyA;
-    const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
-    const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
-    const int jb0 = r0 + (int)(((int64_t)yy * nr) / ny);
-    const int jb1 = r0 + (int)(((int64_t)(yy + 1) * nr) / ny);
-    if (jb0 >= jb1) return;  // uniform over the block
-
-    __shared__ __attribute__((aligned(16))) T sp[RP][WL];
-    __shared__ __attribute__((aligned(16))) T sz[RZ][WL];
-    __shared__ __attribute__((aligned(16))) T sl[RL][WL];
 
     const T *psi = a.psi[layer];
     const T *zeta = a.zeta[layer];
@@ -466,6 +473,7 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
     const bool small = M < W + 4;
 
     auto wx = [&](int x) -> int {
+        if constexpr (!EDGE) return x;
         if (small) return ((x % M) + M) % M;
         return x < 0 ? x + M : (x >= M ? x - M : x);
     };
@@ -475,7 +483,7 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
     };
     const int hq = t == 0 ? 0 : (t == TX - 1 ? W + 2 : -1);  // halo pair LDS index, or none
     const int xh = t == 0 ? x0 - 2 : x0 + W;
-    const bool has_a = xa < M, has_b = xa + 1 < M;
+    const bool has_a = !EDGE || xa < M, has_b = !EDGE || xa + 1 < M;
     const bool ab3 = a.ab3 != 0;
     const int c0 = 2 * t + 2;  // LDS index of xa
 
@@ -488,7 +496,12 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
         }
     };
     auto load_halo = [&](const T *r, V &h) {
-        if (hq >= 0) h = V{r[wx(xh)], r[wx(xh + 1)]};
+        if constexpr (EDGE) {
+            if (hq >= 0) h = V{r[wx(xh)], r[wx(xh + 1)]};
+        } else if (hq >= 0) {
+            const VU v = *(const VU *)(r + xh);
+            h = V{v.x, v.y};
+        }
     };
     // prefetch pipeline PF rows deep: slot 0 is consumed next
     V pc[PF], ph[PF], zc[PF], zh[PF], f1[PF], f2[PF];
@@ -645,19 +658,42 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
                                : zcen + (dtT * F);
                 out_f[v] = F;
             }
-            store_pair_with_ghosts(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, xa, out_z[0],
-                                   out_z[1], has_b);
-            store_pair_with_ghosts(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, xa, out_f[0],
-                                   out_f[1], has_b);
+            store_pair_with_ghosts<T, EDGE>(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, xa,
+                                            out_z[0], out_z[1], has_b);
+            store_pair_with_ghosts<T, EDGE>(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, xa,
+                                            out_f[0], out_f[1], has_b);
             if (ab3 && a.fshift1[layer]) {  // (see TendArgsT::fshift1)
                 T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
-                store_pair_with_ghosts(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, xa, f1c.x,
-                                       f1c.y, has_b);
-                store_pair_with_ghosts(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, xa, f2c.x,
-                                       f2c.y, has_b);
+                store_pair_with_ghosts<T, EDGE>(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, xa,
+                                                f1c.x, f1c.y, has_b);
+                store_pair_with_ghosts<T, EDGE>(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, xa,
+                                                f2c.x, f2c.y, has_b);
             }
         }
     }
+}
+
+// PF: register prefetch depth in rows (as tendency_kernel's)
+template <int TX, class T, int PF = 1>
+__global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int nyA, int nyB) {
+    constexpr int RP = 6, RZ = 5, RL = 4, W = 2 * TX, WL = W + 4;
+    const TendBlock tb = tend_block();
+    const int M = (int)a.M;
+    const int x0 = tb.x * W;
+    const int y = tb.y;
+    const bool second = y >= nyA;
+    const int r0 = second ? a.j2 : a.j0, nr = second ? a.j3 - a.j2 : a.j1 - a.j0;
+    const int yy = second ? y - nyA : y, ny = second ? nyB : nyA;
+    const int jb0 = r0 + (int)(((int64_t)yy * nr) / ny);
+    const int jb1 = r0 + (int)(((int64_t)(yy + 1) * nr) / ny);
+    if (jb0 >= jb1) return;  // uniform over the block
+    __shared__ __attribute__((aligned(16))) T sp[RP][WL];
+    __shared__ __attribute__((aligned(16))) T sz[RZ][WL];
+    __shared__ __attribute__((aligned(16))) T sl[RL][WL];
+    if (x0 >= 2 && x0 + W + 2 <= M)  // (uniform) the x-halo inside the row
+        tendency_pair_strip<TX, T, PF, false>(a, tb.z, x0, jb0, jb1, sp, sz, sl);
+    else
+        tendency_pair_strip<TX, T, PF, true>(a, tb.z, x0, jb0, jb1, sp, sz, sl);
 }
 
 // ------------------------------------------------------------------------------------

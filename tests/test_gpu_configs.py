@@ -267,14 +267,16 @@ def test_config5_eight_8192_f32_slabs_smooth_field(env, capsys):
     slabs = _run_slabs(torch, qgamd, ThreadRing, m, G, steps, torch.float32, init=init)
     glob.run(1, steps)
     torch.cuda.synchronize()
-    worst = _compare_slabs(torch, glob, slabs, {"zeta": SLAB_TOL_F32_SMOOTH, "f_store": SLAB_TOL_F32_SMOOTH,
-                                                "psi": SLAB_TOL_F32_SMOOTH})
+    worst = _compare_slabs(torch, glob, slabs, {"psi": PSI_TOL_F32_SMOOTH, "zeta": ZETA_TOL_F32_SMOOTH,
+                                                "f_store": ZETA_TOL_F32_SMOOTH})
     with capsys.disabled():
         print(f"\nconfig 5 (8 x 8192^2 F32 slabs vs one GPU, smooth field, {steps} steps): worst rel diff {worst}")
 
 
-# set from the first measurement (r04): a smooth field keeps psi at F32 accuracy
-SLAB_TOL_F32_SMOOTH = 1e-5
+# bars: the smooth-field F32 bars above.  Measured (r04, 3 steps): psi 3.4e-7 -- F32 accuracy,
+# against 2.5e-3 on the white-noise field -- and zeta 1.2e-5, F 4.5e-5: the slabs' psi differs
+# from one GPU's by F32 roundoff with grid-scale structure, which nu del^4 psi lifts relative
+# to the smooth tendency (the mechanism of test_config5_f32_smooth_field)
 
 
 @pytest.mark.parametrize("G,M,P,dtype", [(2, 64, 64, "f64"), (3, 48, 96, "f64"), (4, 64, 128, "f32")])
