@@ -6,10 +6,8 @@
 #include <cstring>
 #include <type_traits>
 #include <vector>
-#include <cstdio>
 #include <memory>
 #include <new>
-#include <string>
 
 #include "qg_common.hpp"
 #include "qg_pcg.hpp"
@@ -79,12 +77,10 @@ struct qg_ctx {
     bool graph_ok = true;  // cleared if capture fails (then qg_run launches step by step)
     hipStream_t gstream = nullptr;
     hipEvent_t gev_in = nullptr, gev_out = nullptr;
-    // halo / interior overlap (qg_set_overlap): exchange stream, "fields ready" and "halo in";
-    // the interior rows run on ov_int, a stream whose CU mask leaves some CUs to the exchange
-    // kernels (ov_int = nullptr: on the context's stream)
+    // halo / interior overlap (qg_set_overlap): exchange stream, "fields ready" and "halo in"
     bool overlap = false;
-    hipStream_t ov_stream = nullptr, ov_int = nullptr;
-    hipEvent_t ov_ready = nullptr, ov_halo = nullptr, ov_int_done = nullptr;
+    hipStream_t ov_stream = nullptr;
+    hipEvent_t ov_ready = nullptr, ov_halo = nullptr;
     hipEvent_t pace_ev = nullptr;  // multi-GPU pacing (qg_step)
     bool pace_armed = false;
     int64_t pace_count = 0;
@@ -250,12 +246,9 @@ int qg_destroy(qg_ctx *c) {
     if (c->ov_stream) (void)hipStreamSynchronize(c->ov_stream);
     if (c->comm) comm_destroy(c->comm);
     if (c->halo) (void)hipFree(c->halo);
-    if (c->ov_int) (void)hipStreamSynchronize(c->ov_int);
     if (c->ov_stream) (void)hipStreamDestroy(c->ov_stream);
-    if (c->ov_int) (void)hipStreamDestroy(c->ov_int);
     if (c->ov_ready) (void)hipEventDestroy(c->ov_ready);
     if (c->ov_halo) (void)hipEventDestroy(c->ov_halo);
-    if (c->ov_int_done) (void)hipEventDestroy(c->ov_int_done);
     if (c->diag) (void)hipFree(c->diag);
     if (c->wind) (void)hipFree(c->wind);
     drop_graphs(c);
@@ -365,58 +358,6 @@ static int flush_ghosts(qg_ctx *c) {
     return QG_OK;
 }
 
-// The halo overlap's streams.  The exchange kernels (pack + RCCL send/recv) need a slot on
-// some CU while the interior rows' tendency runs, and the tendency fills every CU: its
-// workgroups hold each SIMD's VGPRs up to 96 x 4-5 waves of the 512, where the RCCL kernel's
-// waves need 136 (r04 trace: the exchange ran 320 us beside the interior, 14 us alone; LDS
-// room alone did not help).  So the interior rows run on a stream whose CU mask leaves out
-// QG_OV_CUS (a comma list of CU indices, default one CU per XCD) for the exchange.
-static bool ov_room() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = std::getenv("QG_OV_ROOM");
-        v = e ? std::atoi(e) != 0 : 0;
-    }
-    return v != 0;
-}
-static int overlap_streams(qg_ctx *c) {
-    QG_HIP(hipStreamCreateWithFlags(&c->ov_stream, hipStreamNonBlocking));
-    QG_HIP(hipEventCreateWithFlags(&c->ov_ready, hipEventDisableTiming));
-    QG_HIP(hipEventCreateWithFlags(&c->ov_halo, hipEventDisableTiming));
-    QG_HIP(hipEventCreateWithFlags(&c->ov_int_done, hipEventDisableTiming));
-    int cus = 0;
-    QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0u);
-    for (int k = 0; k < cus; ++k) mask[k / 32] |= 1u << (k % 32);
-    std::string spec = "0,32,64,96,128,160,192,224";
-    if (const char *e = std::getenv("QG_OV_CUS")) spec = e;
-    int excluded = 0;
-    for (size_t pos = 0; pos < spec.size();) {
-        const size_t q = spec.find(',', pos);
-        const int k = std::atoi(spec.substr(pos, q == std::string::npos ? std::string::npos : q - pos).c_str());
-        if (k >= 0 && k < cus && (mask[k / 32] >> (k % 32) & 1u)) {
-            mask[k / 32] &= ~(1u << (k % 32));
-            ++excluded;
-        }
-        if (q == std::string::npos) break;
-        pos = q + 1;
-    }
-    // (the mask size is in 32-bit words)
-    if (excluded > 0 && excluded < cus)
-        QG_HIP(hipExtStreamCreateWithCUMask(&c->ov_int, (uint32_t)mask.size(), mask.data()));
-    if (std::getenv("QG_OCC_VERBOSE")) {
-        std::fprintf(stderr, "overlap: interior stream leaves %d of %d CUs to the exchange;", c->ov_int ? excluded : 0,
-                     cus);
-        if (c->ov_int) {
-            std::vector<uint32_t> got(mask.size(), 0u);
-            QG_HIP(hipExtStreamGetCUMask(c->ov_int, (uint32_t)got.size(), got.data()));
-            for (uint32_t w : got) std::fprintf(stderr, " %08x", w);
-        }
-        std::fprintf(stderr, "\n");
-    }
-    return QG_OK;
-}
-
 extern "C++" {
 template <class T>
 static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
@@ -506,7 +447,11 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
             // context's stream (the previous step's pass B, a ghost flush using the staging
             // buffer); the interior rows [2, P-2) read only local rows -- no halo, no ghost
             // row -- and write rows the unpack never touches, so they run meanwhile
-            if (!c->ov_stream) QG_CHECK(overlap_streams(c));
+            if (!c->ov_stream) {
+                QG_HIP(hipStreamCreateWithFlags(&c->ov_stream, hipStreamNonBlocking));
+                QG_HIP(hipEventCreateWithFlags(&c->ov_ready, hipEventDisableTiming));
+                QG_HIP(hipEventCreateWithFlags(&c->ov_halo, hipEventDisableTiming));
+            }
             QG_HIP(hipEventRecord(c->ov_ready, c->stream));
             QG_HIP(hipStreamWaitEvent(c->ov_stream, c->ov_ready, 0));
             QG_CHECK(comm_halo_rows(c->comm, f2, 4, c->row_words(), p.P, c->ov_stream, hr));
@@ -516,14 +461,7 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
             in.j0 = 2;
             in.j1 = (int)p.P - 2;
             in.j2 = in.j3 = 0;
-            if (c->ov_int) {
-                QG_HIP(hipStreamWaitEvent(c->ov_int, c->ov_ready, 0));
-                QG_CHECK(launch_tendency(in, c->ov_int, ov_room()));
-                QG_HIP(hipEventRecord(c->ov_int_done, c->ov_int));
-                QG_HIP(hipStreamWaitEvent(c->stream, c->ov_int_done, 0));
-            } else {
-                QG_CHECK(launch_tendency(in, c->stream, ov_room()));
-            }
+            QG_CHECK(launch_tendency(in, c->stream));
             QG_HIP(hipStreamWaitEvent(c->stream, c->ov_halo, 0));
             TendArgsT<T> bd = a;  // rows 0, 1 and P-2, P-1: one launch, two row ranges
             bd.j0 = 0;

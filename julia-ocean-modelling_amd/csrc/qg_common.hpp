@@ -50,6 +50,35 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
 }
 __device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
 __device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
+// the same on float2 (the F32-arithmetic transforms of the F32 wide-row solver)
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// component type of a complex vector type
+template <class C>
+struct CxReal;
+template <>
+struct CxReal<double2> {
+    using R = double;
+};
+template <>
+struct CxReal<float2> {
+    using R = float;
+};
+template <class C>
+__device__ __forceinline__ C cmake(typename CxReal<C>::R x, typename CxReal<C>::R y) {
+    C c;
+    c.x = x;
+    c.y = y;
+    return c;
+}
+// conversions between the storage / arithmetic complex types
+__device__ __forceinline__ void cconv(double2 &d, double2 s) { d = s; }
+__device__ __forceinline__ void cconv(float2 &d, double2 s) { d = make_float2((float)s.x, (float)s.y); }
+__device__ __forceinline__ void cconv(double2 &d, float2 s) { d = make_double2(s.x, s.y); }
+__device__ __forceinline__ void cconv(float2 &d, float2 s) { d = s; }
 
 // Streaming accesses (read or written once per step; non-temporal variants measured no gain).
 template <class T>
@@ -207,10 +236,8 @@ inline double wind_row(double tau0, double rho0, double H1, double dx, int64_t P
     return -A * std::sin(pi2 * (((double)jg + 0.5) / (double)P_total));
 }
 
-// room = true: every CU keeps OVERLAP_LDS_ROOM bytes of LDS free while this launch runs (the
-// halo overlap's interior rows: the exchange kernel on the side stream needs a slot beside them)
-int launch_tendency(const TendArgsT<double> &a, hipStream_t s, bool room = false);
-int launch_tendency(const TendArgsT<float> &a, hipStream_t s, bool room = false);
+int launch_tendency(const TendArgsT<double> &a, hipStream_t s);
+int launch_tendency(const TendArgsT<float> &a, hipStream_t s);
 // the same tendency, both layers per workgroup, also certifying the previous solve (a.cert):
 // *nblk = workgroups launched (partials written); a grid of more than `cap` workgroups (the
 // partials' capacity) is refused before anything is launched

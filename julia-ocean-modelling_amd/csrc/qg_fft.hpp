@@ -15,13 +15,20 @@
 // k < NS; passes with NS > 256 use a two-level table (64 low + NS/64 high entries, one
 // complex multiply to combine).
 //
+// C: the complex type the transform computes and stores in -- double2 (default), or float2
+// for the F32-state wide-row solver (half the LDS bytes and registers, F32 arithmetic; the
+// twiddles are the F64 table rounded once).
+//
 // LDS layouts: a pass with stride NS < 8 scatters with a lane stride of NS*16 B, which
 // conflicts in the 8-lane groups of ds_write_b128; its output buffer is XOR-swizzled within
 // aligned 8-element blocks, x ^ ((x >> 3) & 7).  That is conflict-free both for those writes
 // and for the next pass's contiguous ds_read_b128 (16-lane groups, 64 banks); a pad slot per 8
 // values (the layout before) fixed the writes but left those reads 2-way conflicted: 256
 // extra LDS cycles per 4096-point row, measured as SQ_LDS_BANK_CONFLICT in the wide-row passes
-// (tools/lds_bank_model.py models both).  All other buffers (caller-written rows, wide-stride
+// (tools/lds_bank_model.py models both).  8-byte elements (float2) are banked in 16-lane
+// groups of 16 slots: x ^ ((x >> 4) & 7) keeps both the scattered writes and the contiguous
+// reads distinct there, and the stride-8 pass (whose 16-lane groups span two 8-lane runs 64
+// elements apart) flips bit 3 by bit 6.  All other buffers (caller-written rows, wide-stride
 // pass outputs) are read and written contiguously and use the identity layout.
 #pragma once
 
@@ -29,37 +36,38 @@
 
 namespace qg {
 
-template <bool INV>
-__device__ __forceinline__ double2 mul_mi(double2 a) {  // a * (-i) forward, a * (+i) inverse
-    return INV ? make_double2(-a.y, a.x) : make_double2(a.y, -a.x);
+template <bool INV, class C>
+__device__ __forceinline__ C mul_mi(C a) {  // a * (-i) forward, a * (+i) inverse
+    return INV ? cmake<C>(-a.y, a.x) : cmake<C>(a.y, -a.x);
 }
 
-template <bool INV>
-__device__ __forceinline__ void dft2(double2 &a0, double2 &a1) {
-    const double2 t = a0;
+template <bool INV, class C>
+__device__ __forceinline__ void dft2(C &a0, C &a1) {
+    const C t = a0;
     a0 = cadd(t, a1);
     a1 = csub(t, a1);
 }
 
-template <bool INV>
-__device__ __forceinline__ void dft4(double2 &a0, double2 &a1, double2 &a2, double2 &a3) {
-    const double2 t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = mul_mi<INV>(csub(a1, a3));
+template <bool INV, class C>
+__device__ __forceinline__ void dft4(C &a0, C &a1, C &a2, C &a3) {
+    const C t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = cadd(a1, a3), t3 = mul_mi<INV>(csub(a1, a3));
     a0 = cadd(t0, t2);
     a2 = csub(t0, t2);
     a1 = cadd(t1, t3);
     a3 = csub(t1, t3);
 }
 
-template <bool INV>
-__device__ __forceinline__ void dft8(double2 (&v)[8]) {
-    constexpr double h = 0.70710678118654752440;
-    double2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
-    double2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+template <bool INV, class C>
+__device__ __forceinline__ void dft8(C (&v)[8]) {
+    using R = typename CxReal<C>::R;
+    constexpr R h = (R)0.70710678118654752440;
+    C e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+    C o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
     dft4<INV>(e0, e1, e2, e3);
     dft4<INV>(o0, o1, o2, o3);
     // twiddles W8^k, W8 = exp(-+ i pi/4)
-    const double2 w1 = INV ? make_double2(h, h) : make_double2(h, -h);
-    const double2 w3 = INV ? make_double2(-h, h) : make_double2(-h, -h);
+    const C w1 = INV ? cmake<C>(h, h) : cmake<C>(h, -h);
+    const C w3 = INV ? cmake<C>(-h, h) : cmake<C>(-h, -h);
     o1 = cmul(o1, w1);
     o2 = mul_mi<INV>(o2);
     o3 = cmul(o3, w3);
@@ -73,8 +81,8 @@ __device__ __forceinline__ void dft8(double2 (&v)[8]) {
     v[7] = csub(e3, o3);
 }
 
-template <int R, bool INV>
-__device__ __forceinline__ void dftR(double2 (&v)[R]) {
+template <int R, bool INV, class C>
+__device__ __forceinline__ void dftR(C (&v)[R]) {
     if constexpr (R == 2) dft2<INV>(v[0], v[1]);
     else if constexpr (R == 4) dft4<INV>(v[0], v[1], v[2], v[3]);
     else dft8<INV>(v);
@@ -90,9 +98,11 @@ struct PassRadix {
 };
 
 __host__ __device__ constexpr int lpad(int x) { return x + (x >> 3); }
-template <int NS>  // layout of the buffer written by the pass with stride NS (caller: NS = 0)
+// layout of the buffer written by the pass with stride NS (caller: NS = 0); EB = element bytes
+template <int NS, int EB = 16>
 __device__ __forceinline__ int lay(int x) {
-    if constexpr (NS > 0 && NS < 8) return x ^ ((x >> 3) & 7);
+    if constexpr (NS > 0 && NS < 8) return EB == 16 ? x ^ ((x >> 3) & 7) : x ^ ((x >> 4) & 7);
+    else if constexpr (NS == 8 && EB == 8) return x ^ (((x >> 6) & 1) << 3);
     else return x;
 }
 template <int N>
@@ -136,8 +146,8 @@ struct FftPlan {
     static constexpr int tw_off() { return P::tw_total - Passes<N, T, NS>::tw_total; }
 };
 
-template <int N, int T, int NS>
-__device__ __forceinline__ void fill_twiddles(double2 *twl, const double2 *__restrict__ tw, int t) {
+template <int N, int T, int NS, class C>
+__device__ __forceinline__ void fill_twiddles(C *twl, const double2 *__restrict__ tw, int t) {
     if constexpr (NS < N) {
         using P = Passes<N, T, NS>;
         constexpr int R = P::R, S = N / (NS * R), off = FftPlan<N, T>::template tw_off<NS>();
@@ -146,7 +156,7 @@ __device__ __forceinline__ void fill_twiddles(double2 *twl, const double2 *__res
                 int m;
                 if constexpr (NS <= 256) m = e * S;
                 else m = e < 64 ? e * S : 64 * (e - 64) * S;
-                twl[off + e] = tw[m];
+                cconv(twl[off + e], tw[m]);
             }
         }
         fill_twiddles<N, T, NS * R>(twl, tw, t);
@@ -154,8 +164,8 @@ __device__ __forceinline__ void fill_twiddles(double2 *twl, const double2 *__res
 }
 
 // Fill the LDS twiddle tables (caller synchronises before the first transform).
-template <int N, int T>
-__device__ __forceinline__ void fft_init_twiddles(double2 *twl, const double2 *__restrict__ tw) {
+template <int N, int T, class C>
+__device__ __forceinline__ void fft_init_twiddles(C *twl, const double2 *__restrict__ tw) {
     fill_twiddles<N, T, 1>(twl, tw, threadIdx.x);
 }
 
@@ -193,26 +203,26 @@ __device__ __forceinline__ void fft_twiddle_load(TwFill<N, T> &f, const double2 
         if (e < TwFill<N, T>::TW) f.v[p] = tw[tw_src<N, T, 1>(e)];
     }
 }
-template <int N, int T>
-__device__ __forceinline__ void fft_twiddle_store(double2 *twl, const TwFill<N, T> &f) {
+template <int N, int T, class C>
+__device__ __forceinline__ void fft_twiddle_store(C *twl, const TwFill<N, T> &f) {
 #pragma unroll
     for (int p = 0; p < TwFill<N, T>::PER; ++p) {
         const int e = threadIdx.x + p * T;
-        if (e < TwFill<N, T>::TW) twl[e] = f.v[p];
+        if (e < TwFill<N, T>::TW) cconv(twl[e], f.v[p]);
     }
 }
 
 // One pass: butterflies j = t, t + T, ...; reads `src` (layout of the writer with stride
 // IN_NS) or registers `io` (FROM_REG), writes `dst` with layout lay<NS> then a barrier, or
 // leaves the result in `io` (TO_REG, no barrier).
-template <int N, int T, int NS, int IN_NS, bool INV, bool FROM_REG, bool TO_REG>
-__device__ __forceinline__ void fft_pass(const double2 *src, double2 *dst, const double2 *twl, int t,
-                                         double2 (&io)[PassRadix<N, T, NS>::value]) {
+template <int N, int T, int NS, int IN_NS, bool INV, bool FROM_REG, bool TO_REG, class C>
+__device__ __forceinline__ void fft_pass(const C *src, C *dst, const C *twl, int t,
+                                         C (&io)[PassRadix<N, T, NS>::value]) {
     constexpr int R = PassRadix<N, T, NS>::value;
     constexpr int NB = N / R;
     constexpr int PER = (NB + T - 1) / T;
     static_assert(!(FROM_REG || TO_REG) || (NB == T), "register I/O needs one butterfly per thread");
-    double2 v[PER][R];
+    C v[PER][R];
 #pragma unroll
     for (int p = 0; p < PER; ++p) {
         const int j = t + p * T;
@@ -221,16 +231,16 @@ __device__ __forceinline__ void fft_pass(const double2 *src, double2 *dst, const
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if constexpr (FROM_REG) v[p][r] = io[r];
-                else v[p][r] = src[lay<IN_NS>(j + r * NB)];
+                else v[p][r] = src[lay<IN_NS, sizeof(C)>(j + r * NB)];
             }
             if constexpr (NS > 1) {
                 constexpr int off = FftPlan<N, T>::template tw_off<NS>();
-                double2 w;
+                C w;
                 if constexpr (NS <= 256) w = twl[off + k];
                 else w = cmul(twl[off + (k & 63)], twl[off + 64 + (k >> 6)]);
                 if (INV) w.y = -w.y;
                 // W^(r k) by repeated multiplication (error <= R eps)
-                double2 wr = w;
+                C wr = w;
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
                     v[p][r] = cmul(v[p][r], wr);
@@ -252,7 +262,7 @@ __device__ __forceinline__ void fft_pass(const double2 *src, double2 *dst, const
                 const int k = j % NS;
                 const int base = (j / NS) * NS * R + k;
 #pragma unroll
-                for (int r = 0; r < R; ++r) dst[lay<NS>(base + r * NS)] = v[p][r];
+                for (int r = 0; r < R; ++r) dst[lay<NS, sizeof(C)>(base + r * NS)] = v[p][r];
             }
         }
         __syncthreads();
@@ -261,15 +271,14 @@ __device__ __forceinline__ void fft_pass(const double2 *src, double2 *dst, const
 
 // Passes NS .. end, ping-ponging src -> dst.  LAST_REG: the final pass leaves its output in
 // `io` (element t + r*T).  Returns nothing; which buffer holds the result is FftRun::final.
-template <int N, int T, int NS, int IN_NS, bool INV, bool LAST_REG>
-__device__ __forceinline__ void fft_run(double2 *src, double2 *dst, const double2 *twl, int t,
-                                        double2 (&io)[FftPlan<N, T>::R_LAST]) {
+template <int N, int T, int NS, int IN_NS, bool INV, bool LAST_REG, class C>
+__device__ __forceinline__ void fft_run(C *src, C *dst, const C *twl, int t, C (&io)[FftPlan<N, T>::R_LAST]) {
     if constexpr (NS < N) {
         constexpr int R = PassRadix<N, T, NS>::value;
         if constexpr (LAST_REG && NS * R >= N) {
             fft_pass<N, T, NS, IN_NS, INV, false, true>(src, dst, twl, t, io);
         } else {
-            double2 dummy[R];
+            C dummy[R];
             fft_pass<N, T, NS, IN_NS, INV, false, false>(src, dst, twl, t, dummy);
             fft_run<N, T, NS * R, NS, INV, LAST_REG>(dst, src, twl, t, io);
         }
@@ -288,7 +297,7 @@ __device__ __forceinline__ int opaque_tid() {
 // Forward/inverse transform whose input row is in b0 (identity layout, written by the caller
 // and synchronised).  Result: registers `io` (element t + r*T) when OUT_REG, else the buffer
 // b0 or b1 named by result_in_b1 with layout lay<LAST_NS>.
-template <int N, int T, bool INV, bool OUT_REG>
+template <int N, int T, bool INV, bool OUT_REG, class C = double2>
 struct FftFromLds {
     using Plan = FftPlan<N, T>;
     // passes that write a buffer: all, or all but the last
@@ -296,24 +305,22 @@ struct FftFromLds {
     static constexpr bool result_in_b1 = Plan::PINGPONG && (WRITES % 2) == 1;
     // buffer read after the last barrier (by the last pass when OUT_REG, else by the caller)
     static constexpr bool b0_read_late = !Plan::PINGPONG || (OUT_REG ? (WRITES % 2 == 0) : !result_in_b1);
-    __device__ static __forceinline__ void run(double2 *b0, double2 *b1, const double2 *twl,
-                                               double2 (&io)[Plan::R_LAST]) {
+    __device__ static __forceinline__ void run(C *b0, C *b1, const C *twl, C (&io)[Plan::R_LAST]) {
         fft_run<N, T, 1, 0, INV, OUT_REG>(b0, b1, twl, opaque_tid(), io);
     }
 };
 
 // Transform whose input is in registers `in` (element t + r*T, needs Plan::REG_IN).  Result
 // in b0 or b1 (result_in_b1) with layout lay<LAST_NS>, synchronised.
-template <int N, int T, bool INV>
+template <int N, int T, bool INV, class C = double2>
 struct FftFromReg {
     using Plan = FftPlan<N, T>;
     static constexpr bool result_in_b1 = Plan::PINGPONG && (Plan::NPASS % 2) == 0;
     static constexpr bool b0_read_late = !result_in_b1;
-    __device__ static __forceinline__ void run(double2 (&in)[Plan::R0], double2 *b0, double2 *b1,
-                                               const double2 *twl) {
+    __device__ static __forceinline__ void run(C (&in)[Plan::R0], C *b0, C *b1, const C *twl) {
         const int t = opaque_tid();
-        fft_pass<N, T, 1, 0, INV, true, false>(nullptr, b0, twl, t, in);
-        double2 dummy[Plan::R_LAST];
+        fft_pass<N, T, 1, 0, INV, true, false>((const C *)nullptr, b0, twl, t, in);
+        C dummy[Plan::R_LAST];
         fft_run<N, T, Plan::R0, 1, INV, false>(b0, b1, twl, t, dummy);
     }
 };

@@ -886,7 +886,29 @@ constexpr int HK = HN / HT;        // wavenumber slots per thread: k = t + q*HT;
                                    // packs the real lines k = 0 (.x) and k = HN (.y)
 using HPlan = FftPlan<HN, HT>;
 static_assert(HPlan::REG_IN && HPlan::PINGPONG && HPlan::R0 == HK, "wide-row plan");
-constexpr int HLDS = HPlan::LDS + 128;  // + two-level split-step twiddles (64 + 64)
+// The transforms compute in the state's precision (HC<S>: float2 for F32 states -- half the
+// LDS bytes of every pass and F32 arithmetic, the passes' bound; the recurrences,
+// chunk summaries, split-step twiddles and the pin stay F64).  LDS: the two row buffers and
+// the pass twiddles in HC<S>, then the two-level split-step twiddles (64 + 64) in F64.
+template <class S>
+using HC = typename std::conditional<sizeof(S) == 4, float2, double2>::type;
+static_assert(((2 * LdsSize<HN>::value + HPlan::TW) * sizeof(float2)) % 16 == 0, "F64 split twiddles aligned");
+template <class S>
+constexpr size_t half_lds_bytes() {
+    return sizeof(HC<S>) * (2 * LdsSize<HN>::value + HPlan::TW) + sizeof(double2) * 128;
+}
+template <class S>
+struct HalfLds {
+    HC<S> *b0, *b1, *twl;
+    double2 *wlo, *whi;
+    __device__ explicit HalfLds(void *base) {
+        b0 = static_cast<HC<S> *>(base);
+        b1 = b0 + LdsSize<HN>::value;
+        twl = b1 + LdsSize<HN>::value;
+        wlo = reinterpret_cast<double2 *>(twl + HPlan::TW);
+        whi = wlo + 64;
+    }
+};
 
 template <class S>
 struct Pair;  // two adjacent row elements (8-byte / 4-byte alignment: rows start at element 1)
@@ -903,7 +925,8 @@ __device__ __forceinline__ double2 half_tw(const double2 *wlo, const double2 *wh
     return cmul(wlo[k & 63], whi[k >> 6]);
 }
 
-__device__ __forceinline__ void half_lds_init(const SpecArgs &a, double2 *twl, double2 *wlo, double2 *whi) {
+template <class C>
+__device__ __forceinline__ void half_lds_init(const SpecArgs &a, C *twl, double2 *wlo, double2 *whi) {
     // every load in flight before the first LDS write (one memory latency, not one per table)
     TwFill<HN, HT> twf;
     fft_twiddle_load<HN, HT>(twf, a.tw2);
@@ -924,11 +947,13 @@ template <class S>
 __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     using US = typename Store<S>::C;
     using PV = typename Pair<S>::V;
-    using Fwd = FftFromReg<HN, HT, false>;
+    using CX = HC<S>;
+    using Fwd = FftFromReg<HN, HT, false, CX>;
     extern __shared__ double2 lds[];
-    double2 *b0 = lds, *b1 = lds + LdsSize<HN>::value, *twl = lds + 2 * LdsSize<HN>::value;
-    double2 *wlo = twl + HPlan::TW, *whi = wlo + 64;
-    const double2 *Zb = Fwd::result_in_b1 ? b1 : b0;
+    const HalfLds<S> hl(lds);
+    CX *b0 = hl.b0, *b1 = hl.b1, *twl = hl.twl;
+    double2 *wlo = hl.wlo, *whi = hl.whi;
+    const CX *Zb = Fwd::result_in_b1 ? b1 : b0;
     half_lds_init(a, twl, wlo, whi);
     __syncthreads();
     // the two workgroups of a chunk read the same input rows: XCD-aware order puts them on
@@ -963,25 +988,26 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     // one row: consume the prefetched row (c1, c2), refill them with row jn (< s0: none)
     auto row_step = [&](int j, PV(&c1)[HK], PV(&c2)[HK], int jn) {
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop
-        double2 in[HK];
+        CX in[HK];
 #pragma unroll
         for (int p = 0; p < HK; ++p)
-            in[p] = make_double2(pa * (double)c1[p].x + pb * (double)c2[p].x,
-                                 pa * (double)c1[p].y + pb * (double)c2[p].y);
+            cconv(in[p], make_double2(pa * (double)c1[p].x + pb * (double)c2[p].x,
+                                      pa * (double)c1[p].y + pb * (double)c2[p].y));
         // first pass from registers, then the next row's loads (in[] is dead by then: fewer
         // live registers than loading first), then the remaining passes
         const int tt = opaque_tid();
-        fft_pass<HN, HT, 1, 0, false, true, false>(nullptr, b0, twl, tt, in);
+        fft_pass<HN, HT, 1, 0, false, true, false>((const CX *)nullptr, b0, twl, tt, in);
         if (jn >= s0) load_row(jn, c1, c2);
         {
-            double2 dummy[HPlan::R_LAST];
+            CX dummy[HPlan::R_LAST];
             fft_run<HN, HT, HPlan::R0, 1, false, false>(b0, b1, twl, tt, dummy);
         }
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
             const int k = t + q * HT;
-            const double2 Zk = Zb[lay<HPlan::LAST_NS>(k)];
+            double2 Zk;
+            cconv(Zk, Zb[lay<HPlan::LAST_NS, sizeof(CX)>(k)]);
             if (k == 0) {  // X_0 = Re + Im, X_HN = Re - Im of Z_0 (both real)
                 const double X0 = Zk.x + Zk.y, XN = Zk.x - Zk.y;
                 if (s == 0) {
@@ -995,7 +1021,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 bw[q] = make_double2(om[q].x * u[q].x + bw[q].x, om[q].y * u[q].y + bw[q].y);
                 om[q] = make_double2(om[q].x * r0, om[q].y * rN);
             } else {
-                const double2 Zm = Zb[lay<HPlan::LAST_NS>(HN - k)];
+                double2 Zm;
+                cconv(Zm, Zb[lay<HPlan::LAST_NS, sizeof(CX)>(HN - k)]);
                 // E = (Z_k + conj Z_{HN-k}) / 2, O = (Z_k - conj Z_{HN-k}) / 2i, X = E + W^k O
                 const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                 const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
@@ -1036,11 +1063,14 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     // half_tmp holds psi~1 in the state's precision (like u: F32 intermediates for F32 states)
     typedef S PD __attribute__((ext_vector_type(2)));  // half_tmp pair (aligned: rows of M)
     constexpr int s = SYS;
+    using CX = HC<S>;
     extern __shared__ double2 lds[];
-    double2 *b0 = lds, *b1 = lds + LdsSize<HN>::value, *twl = lds + 2 * LdsSize<HN>::value;
-    double2 *wlo = twl + HPlan::TW, *whi = wlo + 64;
-    // the split step exchanges X through b1: the first inverse pass writes only b0
-    double2 *Xs = b1;
+    const HalfLds<S> hl(lds);
+    CX *b0 = hl.b0, *b1 = hl.b1, *twl = hl.twl;
+    double2 *wlo = hl.wlo, *whi = hl.whi;
+    // the split step exchanges X through b1 (in the transform's precision: the inverse
+    // transform's input is formed from it): the first inverse pass writes only b0
+    CX *Xs = b1;
     static_assert(HPlan::REG_OUT && HPlan::NPASS == 4, "last pass to registers, reading b0");
     half_lds_init(a, twl, wlo, whi);
     const int t = threadIdx.x, c = blockIdx.x;
@@ -1100,8 +1130,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 #pragma unroll
         for (int p = 0; p < HK; ++p) y1[p] = *reinterpret_cast<const PD *>(yr + 2 * (t + p * HT));
     };
-    // SYS 0: (r, 1/r) of the next row, loaded after this row's stores (off the recurrence's
-    // critical path; the tables do not fit in L1), as in spec_passB.  SYS 1 holds the system-0
+    // SYS 0: (r, 1/r) of the next row, loaded during this row (off the recurrence's critical
+    // path; the tables do not fit in L1), as in spec_passB.  SYS 1 holds the system-0
     // rows in registers and would spill: it re-reads them at the recurrence (8192^2 F64:
     // B0 280 -> 244 us; B1 423 -> 542 us with the early loads)
     constexpr bool EARLY = SYS == 0;
@@ -1138,41 +1168,53 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                 const double2 rr = EARLY ? crq[q] : crr[k];
                 w[q] = cfma(rr.x, w[q], cadd(ul, cu[q]));
                 cu[q] = cscale(cu[q], rr.y);
-                Xs[k] = w[q];
+                cconv(Xs[k], w[q]);
             }
         }
         __syncthreads();
         // Z_k = (X_k + conj X_{HN-k}) + i W^-k (X_k - conj X_{HN-k}); z = IDFT(Z) = x_2n + i x_2n+1
-        double2 in[HK];
+        CX in[HK];
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
             const int k = t + q * HT;
             if (k == 0) {
-                in[q] = make_double2(x0 + w[q].y, x0 - w[q].y);
-            } else {  // X_k = w[q]
-                const double2 Xm = Xs[HN - k];
-                const double2 A = make_double2(w[q].x + Xm.x, w[q].y - Xm.y);
-                const double2 D = make_double2(w[q].x - Xm.x, w[q].y + Xm.y);
+                cconv(in[q], make_double2(x0 + w[q].y, x0 - w[q].y));
+            } else {  // X_k = w[q] (rounded as its partner X_{HN-k} was)
+                double2 Xm, Xk;
+                cconv(Xm, Xs[HN - k]);
+                CX wr;
+                cconv(wr, w[q]);
+                cconv(Xk, wr);
+                const double2 A = make_double2(Xk.x + Xm.x, Xk.y - Xm.y);
+                const double2 D = make_double2(Xk.x - Xm.x, Xk.y + Xm.y);
                 const double2 B = cmul(cconj(half_tw(wlo, whi, k)), D);
-                in[q] = make_double2(A.x - B.y, A.y + B.x);
+                cconv(in[q], make_double2(A.x - B.y, A.y + B.x));
             }
         }
         // first inverse pass, then the next row's loads (in[] dead), then the remaining passes;
         // the last pass leaves its output in registers (element t + p HT: the row order of the
         // stores below), so a row writes the LDS four times (split step + three passes), not five
         const int tt = opaque_tid();
-        fft_pass<HN, HT, 1, 0, true, true, false>(nullptr, b0, twl, tt, in);
+        fft_pass<HN, HT, 1, 0, true, true, false>((const CX *)nullptr, b0, twl, tt, in);
         if (j < e) load_u(j + 1);
         if constexpr (SYS == 1) load_y(j);
-        double2 xo[HPlan::R_LAST];
+        CX xo[HPlan::R_LAST];
         fft_run<HN, HT, HPlan::R0, 1, true, true>(b0, b1, twl, tt, xo);
+        // SYS 0: the next row's (r, 1/r) before this row's stores -- vmcnt counts loads and
+        // stores in order, so loaded after them the next recurrence waited for every store of
+        // this row (8192^2 F32 B0: 187 -> 179 us; the 4096-point pass B, at its register
+        // limit, spills and slows with the same move: 128.5 -> 145.4 us, r04c)
+        if constexpr (EARLY) {
+            if (j < e) load_coef();
+        }
         if constexpr (SYS == 0) {
             S *yr = static_cast<S *>(a.half_tmp) + (size_t)j * a.M;
             const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
 #pragma unroll
             for (int p = 0; p < HK; ++p) {
                 const int n = t + p * HT;
-                const double2 z = xo[p];
+                double2 z;
+                cconv(z, xo[p]);
                 PD v;
                 // the pinned unknown is exactly 0 (get_poisson_cholesky's identity row)
                 v.x = (S)((pin_row && n == 0) ? 0.0 : z.x - pin);
@@ -1199,7 +1241,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 #pragma unroll
             for (int p = 0; p < HK; ++p) {
                 const int n = t + p * HT;
-                const double2 z = xo[p];
+                double2 z;
+                cconv(z, xo[p]);
                 const double x1a = (double)y1[p].x, x1b = (double)y1[p].y;
                 PV v1;
                 v1.x = (S)(a.pin_out[0] * x1a + a.pin_out[1] * z.x);
@@ -1213,10 +1256,6 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                 }
             }
         }
-        if constexpr (EARLY) {
-            asm volatile("" ::: "memory");
-            if (j < e) load_coef();
-        }
         // (no barrier: the last pass read b0, and the next row's first write of b0 follows the
         // split step's barrier; b1, which the next split step writes, was last read by the
         // third pass, before its own barrier)
@@ -1225,7 +1264,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 
 template <class S>
 static int launch_half_t(bool passB, const SpecArgs &a, hipStream_t s) {
-    const size_t lds = sizeof(double2) * HLDS;
+    const size_t lds = half_lds_bytes<S>();
     if (passB) {
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -984,40 +984,15 @@ static int launch_tend_variant(const TendArgsT<T> &a, int rows, hipStream_t s) {
     return QG_OK;
 }
 
-// Resident workgroups per chip (CUs x per-CU occupancy) of a tendency kernel, and the dynamic
-// LDS pad of its launches.  room: each workgroup's LDS is padded so that every CU keeps
-// OVERLAP_LDS_ROOM bytes free -- the halo overlap's exchange kernel (RCCL send/recv, 20 KB of
-// LDS per workgroup) then finds a slot beside the interior rows at once; without the pad the
-// tendency fills the LDS of every CU (5 x 31 KB at 4096^2 F64) and the exchange kernel ran
-// 310 us beside it instead of 14 (r03 trace, profiles/r03/overlap/).
-constexpr int OVERLAP_LDS_ROOM = 24 * 1024;
-struct TendOcc {
-    int slots = 0;
-    unsigned pad = 0;
-};
+// Resident workgroups per chip (CUs x per-CU occupancy) of a tendency kernel
 template <class K>
-static int tend_occupancy(K kernel, int threads, bool room, TendOcc &o) {
-    if (o.slots) return QG_OK;
+static int tend_slots(K kernel, int threads, int &sl) {
+    if (sl) return QG_OK;
     int dev = 0, cus = 0, per = 0;
     QG_HIP(hipGetDevice(&dev));
     QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    unsigned pad = 0;
-    if (room) {
-        int lds_cu = 0;
-        hipFuncAttributes fa{};
-        QG_HIP(hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kernel)));
-        QG_HIP(hipDeviceGetAttribute(&lds_cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev));
-        if (lds_cu < 160 * 1024) lds_cu = 160 * 1024;  // (gfx950: 160 KB per CU)
-        const int st = std::max(1, (int)fa.sharedSizeBytes), avail = lds_cu - OVERLAP_LDS_ROOM;
-        const int n = std::max(1, avail / st);      // workgroups per CU that leave the room
-        const int per_wg = avail / n / 512 * 512;   // stretched to the room's edge
-        pad = per_wg > st ? (unsigned)(per_wg - st) : 0u;
-    }
-    QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, pad));
-    o.slots = cus * (per > 0 ? per : 1);
-    o.pad = pad;
-    if (std::getenv("QG_OCC_VERBOSE"))
-        std::fprintf(stderr, "tendency occupancy: %d per CU (dynamic LDS pad %u, room %d)\n", per, pad, (int)room);
+    QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0));
+    sl = cus * (per > 0 ? per : 1);
     return QG_OK;
 }
 
@@ -1027,12 +1002,10 @@ static int tend_occupancy(K kernel, int threads, bool room, TendOcc &o) {
 // least 4 rows per strip.  (4096^2: 0.380 ms vs 0.385 for fixed 64-row strips; 1024^2: 33 vs
 // 38 us.)
 template <class T>
-static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s, bool room) {
+static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     constexpr int TX = 256, PF = 1;  // register prefetch depth (rows)
-    static TendOcc occ[2];
-    TendOcc &o = occ[room];
-    QG_CHECK(tend_occupancy(tendency_kernel<TX, PF, T>, TX, room, o));
-    const int sl = o.slots;
+    static int sl = 0;
+    QG_CHECK(tend_slots(tendency_kernel<TX, PF, T>, TX, sl));
     static int env_waves = -1;
     if (env_waves < 0) {
         const char *e = std::getenv("QG_TEND_WAVES");
@@ -1053,7 +1026,7 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s, bool room)
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
     dim3 grid((unsigned)nx, (unsigned)(nyA + nyB), 2);
-    tendency_kernel<TX, PF, T><<<grid, TX, o.pad, s>>>(a, nyA, nyB);
+    tendency_kernel<TX, PF, T><<<grid, TX, 0, s>>>(a, nyA, nyB);
     QG_LAUNCH_CHECK();
     return QG_OK;
 }
@@ -1136,12 +1109,10 @@ int launch_tendency_cert(const TendArgsT<double> &a, int64_t cap, int *nblk, hip
 // Float32 default: the pair kernel over whole chip-fulls of 512-point strips (as above);
 // QG_TEND_PAIR=0 selects the one-point kernel instead.
 template <int TX, class T>
-static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s, bool room) {
+static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
     constexpr int W = 2 * TX, PF = 1;
-    static TendOcc occ[2];
-    TendOcc &o = occ[room];
-    QG_CHECK(tend_occupancy(tendency_pair_kernel<TX, T, PF>, TX, room, o));
-    const int sl = o.slots;
+    static int sl = 0;
+    QG_CHECK(tend_slots(tendency_pair_kernel<TX, T, PF>, TX, sl));
     const char *e = std::getenv("QG_TEND_WAVES");
     const int nx = (int)((a.M + W - 1) / W);
     // four chip-fulls at 8192^2 and up (tools/tend_waves_f32.sh: 797 -> 766 us)
@@ -1154,7 +1125,7 @@ static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s, bool room) {
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
     dim3 grid((unsigned)nx, (unsigned)(nyA + nyB), 2);
-    tendency_pair_kernel<TX, T, PF><<<grid, TX, o.pad, s>>>(a, nyA, nyB);
+    tendency_pair_kernel<TX, T, PF><<<grid, TX, 0, s>>>(a, nyA, nyB);
     QG_LAUNCH_CHECK();
     return QG_OK;
 }
@@ -1214,7 +1185,7 @@ static int tend_direct_env() {
 }
 
 template <class T>
-static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s, bool room) {
+static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
     if (a.j1 - a.j0 <= 0 && a.j3 - a.j2 <= 0) return QG_OK;
     int tw, tr;
     tend_tile(tw, tr);
@@ -1226,7 +1197,7 @@ static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s, bool room) {
         default: break;
     }
     if constexpr (sizeof(T) == 4) {
-        if (tend_variant() == 0 && tw == 0 && tend_pair_enabled() && a.M % 2 == 0) return launch_tend_pair<256>(a, s, room);
+        if (tend_variant() == 0 && tw == 0 && tend_pair_enabled() && a.M % 2 == 0) return launch_tend_pair<256>(a, s);
     }  // (F64 pair kernel measured slower: 0.41-0.43 vs 0.386 ms at 4096^2 -- HBM-bound already)
     if (tend_variant() == 0 && tw == 0) {
         const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
@@ -1249,12 +1220,12 @@ static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s, bool room) {
             while (rows > 4 && nx * 2 * ((rows_total + rows - 1) / rows) < 2048) rows >>= 1;
             return launch_tend_variant<256, 1, T>(a, rows, s);
         }
-        default: return launch_tend_balanced(a, s, room);
+        default: return launch_tend_balanced(a, s);
     }
 }
 
-int launch_tendency(const TendArgsT<double> &a, hipStream_t s, bool room) { return launch_tendency_t(a, s, room); }
-int launch_tendency(const TendArgsT<float> &a, hipStream_t s, bool room) { return launch_tendency_t(a, s, room); }
+int launch_tendency(const TendArgsT<double> &a, hipStream_t s) { return launch_tendency_t(a, s); }
+int launch_tendency(const TendArgsT<float> &a, hipStream_t s) { return launch_tendency_t(a, s); }
 
 // seeded initialise_model; P = local rows, P_total / j_offset place the slab in the global grid
 int launch_initialise_global(void *zeta, void *psi, void *f_store, int esize, int64_t M, int64_t P,

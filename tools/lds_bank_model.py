@@ -41,14 +41,25 @@ def extra(addrs, groups, mod):
     return tot
 
 
-def plan(N, T, small_layout):
+def xsw8(x):
+    return x ^ ((x >> 4) & 7)
+
+
+def sw8_ns8(x):
+    return x ^ (((x >> 6) & 1) << 3)
+
+
+RG16 = [list(range(16 * g, 16 * g + 16)) for g in range(4)]
+
+
+def plan(N, T, small_layout, eb=16):
     out = []
     NS = 1
     prev_lay = ident  # the caller's row: identity
     while NS < N:
         R = radix(N, T, NS)
         NB = N // R
-        lay = small_layout if NS < 8 else ident
+        lay = small_layout if NS < 8 else (sw8_ns8 if (eb == 8 and NS == 8 and small_layout is xsw8) else ident)
         wx = rx = 0
         for p in range((NB + T - 1) // T):
             for w0 in range(0, T, 64):
@@ -61,8 +72,12 @@ def plan(N, T, small_layout):
                         rd[lane] = prev_lay(j + r * NB)
                         k = j % NS
                         wr[lane] = lay((j // NS) * NS * R + k + r * NS)
-                    rx += extra(rd, RG, 16)
-                    wx += extra(wr, WG, 8)
+                    if eb == 16:  # ds_read_b128 / ds_write_b128
+                        rx += extra(rd, RG, 16)
+                        wx += extra(wr, WG, 8)
+                    else:  # 8-byte elements: ds_read2_b64 / ds_write_b64 groups (16 lanes, 16 slots)
+                        rx += extra(rd, RG16, 16)
+                        wx += extra(wr, RG16, 16)
         out.append((NS, R, rx, wx))
         prev_lay = lay
         NS *= R
@@ -73,6 +88,6 @@ if __name__ == "__main__":
     cases = [(int(a), int(b)) for a, b in (s.split("x") for s in sys.argv[1:])] or \
         [(4096, 512), (2048, 256), (1024, 256), (512, 128), (256, 64), (128, 64), (8192, 1024), (16, 64), (64, 64)]
     for N, T in cases:
-        for name, lay in (("lpad", lpad), ("xor", xsw)):
-            rows = plan(N, T, lay)
+        for name, lay, eb in (("lpad", lpad, 16), ("xor", xsw, 16), ("xor8", xsw8, 8), ("xor-", xsw, 8)):
+            rows = plan(N, T, lay, eb)
             print(f"N {N:5d} T {T:4d} {name:4s}: " + "  ".join(f"NS{ns}/R{r}: rd+{rx} wr+{wx}" for ns, r, rx, wx in rows))

@@ -25,7 +25,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/$O/trace -o ov -- python3 $R/bench.py --comm-self --overlap --steps 30 --warmup 10 --pcg-steps 0 --dropin-steps 0 --cpu-steps 0 --comm-probe-reps 0 > $R/$O/trace.log 2>&1 || exit 4
 python3 $R/tools/timeline.py $R/$O/trace/ov_kernel_trace.csv spec_carry 3 > $R/$O/timeline.txt
 head -24 $R/$O/timeline.txt
-for v in nopeel cur; do
+for v in nopeel coefearly cur; do
   L=""; [ $v != cur ] && L=$R/julia-ocean-modelling_amd/lib/exp/$v.so
   for n in 8192f32 4096f64; do
     N=${n:0:4}; D=${n:4:3}
