@@ -886,23 +886,34 @@ constexpr int HK = HN / HT;        // wavenumber slots per thread: k = t + q*HT;
                                    // packs the real lines k = 0 (.x) and k = HN (.y)
 using HPlan = FftPlan<HN, HT>;
 static_assert(HPlan::REG_IN && HPlan::PINGPONG && HPlan::R0 == HK, "wide-row plan");
-// The transforms compute in the state's precision (HC<S>: float2 for F32 states -- half the
-// LDS bytes of every pass and F32 arithmetic, the passes' bound; the recurrences,
-// chunk summaries, split-step twiddles and the pin stay F64).  LDS: the two row buffers and
-// the pass twiddles in HC<S>, then the two-level split-step twiddles (64 + 64) in F64.
+// Pass A's forward transform computes in the state's precision (HC<S>: float2 for F32 states
+// -- half the LDS bytes of every pass and F32 arithmetic, the passes' bound); the
+// recurrences, chunk summaries, split-step twiddles and the pin stay F64.  Its rounding enters
+// zeta~'s spectrum, which the solve divides by the operator's eigenvalues (grid-scale errors
+// shrink by ~dx^2 / 8).  Pass B's inverse transform writes psi itself, whose grid-scale
+// rounding the next tendency's nu del^4 psi lifts, so it stays F64 (HCB; QG_HALF_B_F32 builds
+// the F32 form for the measurement).  LDS: the two row buffers and the pass twiddles in the
+// transform's type, then the two-level split-step twiddles (64 + 64) in F64.
 template <class S>
 using HC = typename std::conditional<sizeof(S) == 4, float2, double2>::type;
+#ifdef QG_HALF_B_F32
+template <class S>
+using HCB = HC<S>;
+#else
+template <class S>
+using HCB = double2;
+#endif
 static_assert(((2 * LdsSize<HN>::value + HPlan::TW) * sizeof(float2)) % 16 == 0, "F64 split twiddles aligned");
-template <class S>
+template <class CX>
 constexpr size_t half_lds_bytes() {
-    return sizeof(HC<S>) * (2 * LdsSize<HN>::value + HPlan::TW) + sizeof(double2) * 128;
+    return sizeof(CX) * (2 * LdsSize<HN>::value + HPlan::TW) + sizeof(double2) * 128;
 }
-template <class S>
+template <class CX>
 struct HalfLds {
-    HC<S> *b0, *b1, *twl;
+    CX *b0, *b1, *twl;
     double2 *wlo, *whi;
     __device__ explicit HalfLds(void *base) {
-        b0 = static_cast<HC<S> *>(base);
+        b0 = static_cast<CX *>(base);
         b1 = b0 + LdsSize<HN>::value;
         twl = b1 + LdsSize<HN>::value;
         wlo = reinterpret_cast<double2 *>(twl + HPlan::TW);
@@ -950,7 +961,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     using CX = HC<S>;
     using Fwd = FftFromReg<HN, HT, false, CX>;
     extern __shared__ double2 lds[];
-    const HalfLds<S> hl(lds);
+    const HalfLds<CX> hl(lds);
     CX *b0 = hl.b0, *b1 = hl.b1, *twl = hl.twl;
     double2 *wlo = hl.wlo, *whi = hl.whi;
     const CX *Zb = Fwd::result_in_b1 ? b1 : b0;
@@ -1063,9 +1074,9 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     // half_tmp holds psi~1 in the state's precision (like u: F32 intermediates for F32 states)
     typedef S PD __attribute__((ext_vector_type(2)));  // half_tmp pair (aligned: rows of M)
     constexpr int s = SYS;
-    using CX = HC<S>;
+    using CX = HCB<S>;
     extern __shared__ double2 lds[];
-    const HalfLds<S> hl(lds);
+    const HalfLds<CX> hl(lds);
     CX *b0 = hl.b0, *b1 = hl.b1, *twl = hl.twl;
     double2 *wlo = hl.wlo, *whi = hl.whi;
     // the split step exchanges X through b1 (in the transform's precision: the inverse
@@ -1264,7 +1275,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 
 template <class S>
 static int launch_half_t(bool passB, const SpecArgs &a, hipStream_t s) {
-    const size_t lds = half_lds_bytes<S>();
+    const size_t lds = passB ? half_lds_bytes<HCB<S>>() : half_lds_bytes<HC<S>>();
     if (passB) {
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
