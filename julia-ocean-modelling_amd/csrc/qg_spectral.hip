@@ -886,24 +886,11 @@ constexpr int HK = HN / HT;        // wavenumber slots per thread: k = t + q*HT;
                                    // packs the real lines k = 0 (.x) and k = HN (.y)
 using HPlan = FftPlan<HN, HT>;
 static_assert(HPlan::REG_IN && HPlan::PINGPONG && HPlan::R0 == HK, "wide-row plan");
-// Pass A's forward transform computes in the state's precision (HC<S>: float2 for F32 states
-// -- half the LDS bytes of every pass and F32 arithmetic, the passes' bound); the
-// recurrences, chunk summaries, split-step twiddles and the pin stay F64.  Its rounding enters
-// zeta~'s spectrum, which the solve divides by the operator's eigenvalues (grid-scale errors
-// shrink by ~dx^2 / 8).  Pass B's inverse transform writes psi itself, whose grid-scale
-// rounding the next tendency's nu del^4 psi lifts, so it stays F64 (HCB; QG_HALF_B_F32 builds
-// the F32 form for the measurement).  LDS: the two row buffers and the pass twiddles in the
-// transform's type, then the two-level split-step twiddles (64 + 64) in F64.
-template <class S>
-using HC = typename std::conditional<sizeof(S) == 4, float2, double2>::type;
-#ifdef QG_HALF_B_F32
-template <class S>
-using HCB = HC<S>;
-#else
-template <class S>
-using HCB = double2;
-#endif
-static_assert(((2 * LdsSize<HN>::value + HPlan::TW) * sizeof(float2)) % 16 == 0, "F64 split twiddles aligned");
+// LDS: the two row buffers and the pass twiddles, then the two-level split-step twiddles
+// (64 + 64).  (The transforms stay F64 for F32 states too: computing pass A's in F32 saved
+// 18 of 392 us at 8192^2 and pass B's 16 of 417, while the F32 error grew -- psi 2.3e-3 ->
+// 5.3e-3 against the oracle at 8192 x 16, zeta 1e-4 -> 1e-3 on the smooth field with pass B's
+// in F32 (r04e; qg_fft.hpp keeps the complex type a template parameter).)
 template <class CX>
 constexpr size_t half_lds_bytes() {
     return sizeof(CX) * (2 * LdsSize<HN>::value + HPlan::TW) + sizeof(double2) * 128;
@@ -958,7 +945,7 @@ template <class S>
 __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     using US = typename Store<S>::C;
     using PV = typename Pair<S>::V;
-    using CX = HC<S>;
+    using CX = double2;
     using Fwd = FftFromReg<HN, HT, false, CX>;
     extern __shared__ double2 lds[];
     const HalfLds<CX> hl(lds);
@@ -1002,8 +989,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         CX in[HK];
 #pragma unroll
         for (int p = 0; p < HK; ++p)
-            cconv(in[p], make_double2(pa * (double)c1[p].x + pb * (double)c2[p].x,
-                                      pa * (double)c1[p].y + pb * (double)c2[p].y));
+            in[p] = make_double2(pa * (double)c1[p].x + pb * (double)c2[p].x,
+                                 pa * (double)c1[p].y + pb * (double)c2[p].y);
         // first pass from registers, then the next row's loads (in[] is dead by then: fewer
         // live registers than loading first), then the remaining passes
         const int tt = opaque_tid();
@@ -1017,8 +1004,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
             const int k = t + q * HT;
-            double2 Zk;
-            cconv(Zk, Zb[lay<HPlan::LAST_NS, sizeof(CX)>(k)]);
+            const double2 Zk = Zb[lay<HPlan::LAST_NS>(k)];
             if (k == 0) {  // X_0 = Re + Im, X_HN = Re - Im of Z_0 (both real)
                 const double X0 = Zk.x + Zk.y, XN = Zk.x - Zk.y;
                 if (s == 0) {
@@ -1032,8 +1018,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 bw[q] = make_double2(om[q].x * u[q].x + bw[q].x, om[q].y * u[q].y + bw[q].y);
                 om[q] = make_double2(om[q].x * r0, om[q].y * rN);
             } else {
-                double2 Zm;
-                cconv(Zm, Zb[lay<HPlan::LAST_NS, sizeof(CX)>(HN - k)]);
+                const double2 Zm = Zb[lay<HPlan::LAST_NS>(HN - k)];
                 // E = (Z_k + conj Z_{HN-k}) / 2, O = (Z_k - conj Z_{HN-k}) / 2i, X = E + W^k O
                 const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                 const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
@@ -1074,13 +1059,12 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     // half_tmp holds psi~1 in the state's precision (like u: F32 intermediates for F32 states)
     typedef S PD __attribute__((ext_vector_type(2)));  // half_tmp pair (aligned: rows of M)
     constexpr int s = SYS;
-    using CX = HCB<S>;
+    using CX = double2;
     extern __shared__ double2 lds[];
     const HalfLds<CX> hl(lds);
     CX *b0 = hl.b0, *b1 = hl.b1, *twl = hl.twl;
     double2 *wlo = hl.wlo, *whi = hl.whi;
-    // the split step exchanges X through b1 (in the transform's precision: the inverse
-    // transform's input is formed from it): the first inverse pass writes only b0
+    // the split step exchanges X through b1: the first inverse pass writes only b0
     CX *Xs = b1;
     static_assert(HPlan::REG_OUT && HPlan::NPASS == 4, "last pass to registers, reading b0");
     half_lds_init(a, twl, wlo, whi);
@@ -1179,7 +1163,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                 const double2 rr = EARLY ? crq[q] : crr[k];
                 w[q] = cfma(rr.x, w[q], cadd(ul, cu[q]));
                 cu[q] = cscale(cu[q], rr.y);
-                cconv(Xs[k], w[q]);
+                Xs[k] = w[q];
             }
         }
         __syncthreads();
@@ -1189,17 +1173,13 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
         for (int q = 0; q < HK; ++q) {
             const int k = t + q * HT;
             if (k == 0) {
-                cconv(in[q], make_double2(x0 + w[q].y, x0 - w[q].y));
-            } else {  // X_k = w[q] (rounded as its partner X_{HN-k} was)
-                double2 Xm, Xk;
-                cconv(Xm, Xs[HN - k]);
-                CX wr;
-                cconv(wr, w[q]);
-                cconv(Xk, wr);
-                const double2 A = make_double2(Xk.x + Xm.x, Xk.y - Xm.y);
-                const double2 D = make_double2(Xk.x - Xm.x, Xk.y + Xm.y);
+                in[q] = make_double2(x0 + w[q].y, x0 - w[q].y);
+            } else {  // X_k = w[q]
+                const double2 Xm = Xs[HN - k];
+                const double2 A = make_double2(w[q].x + Xm.x, w[q].y - Xm.y);
+                const double2 D = make_double2(w[q].x - Xm.x, w[q].y + Xm.y);
                 const double2 B = cmul(cconj(half_tw(wlo, whi, k)), D);
-                cconv(in[q], make_double2(A.x - B.y, A.y + B.x));
+                in[q] = make_double2(A.x - B.y, A.y + B.x);
             }
         }
         // first inverse pass, then the next row's loads (in[] dead), then the remaining passes;
@@ -1224,8 +1204,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 #pragma unroll
             for (int p = 0; p < HK; ++p) {
                 const int n = t + p * HT;
-                double2 z;
-                cconv(z, xo[p]);
+                const double2 z = xo[p];
                 PD v;
                 // the pinned unknown is exactly 0 (get_poisson_cholesky's identity row)
                 v.x = (S)((pin_row && n == 0) ? 0.0 : z.x - pin);
@@ -1252,8 +1231,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 #pragma unroll
             for (int p = 0; p < HK; ++p) {
                 const int n = t + p * HT;
-                double2 z;
-                cconv(z, xo[p]);
+                const double2 z = xo[p];
                 const double x1a = (double)y1[p].x, x1b = (double)y1[p].y;
                 PV v1;
                 v1.x = (S)(a.pin_out[0] * x1a + a.pin_out[1] * z.x);
@@ -1275,7 +1253,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
 
 template <class S>
 static int launch_half_t(bool passB, const SpecArgs &a, hipStream_t s) {
-    const size_t lds = passB ? half_lds_bytes<HCB<S>>() : half_lds_bytes<HC<S>>();
+    const size_t lds = half_lds_bytes<double2>();
     if (passB) {
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
