@@ -78,9 +78,11 @@ def parse():
                     help="N > 1: RCCL over xGMI (default), or the host transport over gloo -- a "
                          "rehearsal of the multi-rank bench with several ranks on one GPU (slow, "
                          "not a measurement)")
-    ap.add_argument("--overlap", action="store_true",
+    ap.add_argument("--overlap", dest="overlap", action="store_true", default=True,
                     help="N > 1 (or --comm-self): post the halo exchange on a second stream while the "
-                         "interior rows' tendency runs (qg_set_overlap; bit-identical results)")
+                         "interior rows' tendency runs (qg_set_overlap; bit-identical results; the default)")
+    ap.add_argument("--no-overlap", dest="overlap", action="store_false",
+                    help="N > 1 (or --comm-self): the exchange in stream order before the whole tendency")
     ap.add_argument("--dropin-steps", type=int, default=20,
                     help="also time this many steps through the reference's own array signatures "
                          "(evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(...) on bare arrays, "
@@ -341,8 +343,7 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         st.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
-    if args.overlap:
-        st.set_overlap(True)
+    st.set_overlap(args.overlap)
     st.initialise()
     torch.cuda.synchronize()
     setup_ms = (time.perf_counter() - t_setup) * 1e3

@@ -241,7 +241,9 @@ int qg_comm_set_timeout(qg_ctx *ctx, double seconds);
  * second HIP stream and runs the tendency of the interior rows j in [2, P-2), which need no
  * halo, on the context's stream meanwhile; the four boundary rows follow after an event
  * wait.  Bit-identical to on = 0 (the per-point arithmetic does not depend on the launch
- * geometry).  Default: the environment variable QG_OVERLAP (read at qg_create), else 0.
+ * geometry).  Default: on (the environment variable QG_OVERLAP=0 at qg_create turns it
+ * off): on the 1-rank RCCL ring at 4096^2 it measured 0.5-1.4 % faster than off over three
+ * same-process A/B runs (r04) -- the exchange completes inside the interior's tail.
  * No effect on a single GPU (no exchange) or for P < 8 (no interior worth splitting).   */
 int qg_set_overlap(qg_ctx *ctx, int on);
 /* Time the two collectives of a multi-GPU step in isolation (HIP events on the context's

@@ -78,7 +78,7 @@ struct qg_ctx {
     hipStream_t gstream = nullptr;
     hipEvent_t gev_in = nullptr, gev_out = nullptr;
     // halo / interior overlap (qg_set_overlap): exchange stream, "fields ready" and "halo in"
-    bool overlap = false;
+    bool overlap = true;  // (qg_set_overlap; default on: measured, r04)
     hipStream_t ov_stream = nullptr;
     hipEvent_t ov_ready = nullptr, ov_halo = nullptr;
     hipEvent_t pace_ev = nullptr;  // multi-GPU pacing (qg_step)

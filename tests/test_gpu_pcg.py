@@ -204,15 +204,20 @@ def test_deferred_failure_stops_graph_replay(env, monkeypatch):
 
 
 def test_plain_cg_256(env):
-    """QG_PRECOND_NONE (plain CG) at 256^2, pcg_rtol 1e-12, pcg_maxit 3000: converges (or stops
-    at its roundoff floor <= 1e-10) and matches the oracle; the iteration count is reported."""
+    """QG_PRECOND_NONE (plain CG) at 256^2, pcg_rtol 1e-13, pcg_maxit 3000: converges and
+    matches the oracle at the north-star bar (1e-10).  Measured (r04, tools/cg_floor.py): 965
+    iterations, psi 5.4e-12 from the oracle at 1e-13 (8.7e-11 at 1e-12, 1.0e-12 at 1e-14 and
+    below: the floor); the iteration count is reported."""
     torch, qg, R, O = env
     m = qg.bench_model(256)
-    st = qg.initialise_model(m, solver=1, precond=0, pcg_rtol=1e-12, pcg_maxit=3000)
+    st = qg.initialise_model(m, solver=1, precond=0, pcg_rtol=1e-13, pcg_maxit=3000)
     for t in range(1, 3):
         st.step(t)
         s = st.stats()
         print(f"plain CG 256^2 step {t}: iterations {s['iters']}, relres {s['relres']}")
         assert 1 < s["iters"][0] < 3000 and max(s["relres"]) <= 1e-10, s
     ref = O.State(R.bench_model(256)).run(2)
-    assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-8
+    for n in ("psi", "zeta"):
+        e = np.linalg.norm(getattr(ref, n) - st.to_numpy(n)) / np.linalg.norm(getattr(ref, n))
+        print(f"plain CG 256^2 vs C oracle, {n}: {e:.3e}")
+        assert e < 1e-10, (n, e)
