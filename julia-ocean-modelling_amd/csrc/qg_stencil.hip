@@ -503,10 +503,39 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
             h = V{v.x, v.y};
         }
     };
+    // Ring rows of interior strips 16 B per lane: threads [0, TX/2) read the psi row, [TX/2, TX)
+    // the zeta row, each as (W + 4) / Q vectors of Q elements (x0-2 .. x0+W+1); threads 0 and
+    // TX/2 take the one vector left over each.  One 16-byte load and LDS store per lane and row
+    // instead of two 8-byte ones (a wave's row access touches 9 cache lines per KB instead of
+    // 10 at the rows' element-1 offset): 8192^2 F32 738 -> 725 us (r04h, same box; the walk
+    // alone 0.320 -> 0.311 ms, tools/microbench/strip_width.hip).  The same form for the F64
+    // one-point kernel measured 334.5 -> 336.7 us and is not used.  Ring contents unchanged.
+    constexpr int Q = 16 / sizeof(T);
+    constexpr bool R16 = !EDGE && (W + 4) % Q == 0 && (W + 4) / Q == TX / 2 + 1;
+    typedef T VQ __attribute__((ext_vector_type(Q)));                         // LDS (16-B aligned)
+    typedef T VQU __attribute__((ext_vector_type(Q), aligned(sizeof(T))));  // row (element-1 offset)
+    const bool is_psi = t < TX / 2;  // (wave-uniform for TX % 128 == 0)
+    const int vq = is_psi ? t : t - TX / 2;
+    const bool xtra = t == 0 || t == TX / 2;  // vector TX/2 of its row
+    auto fetch16 = [&](int jp, int jz, VQ &c, VQ &e) {
+        const T *r = (is_psi ? rowp(psi, prs, jp) : rowp(zeta, zrs, jz)) + (x0 - 2);
+        c = *(const VQU *)(r + Q * vq);
+        if (xtra) e = *(const VQU *)(r + Q * (TX / 2));
+    };
+    auto commit16 = [&](int jp, int jz, VQ c, VQ e) {
+        T *d = is_psi ? sp[(jp + 2 * RP) % RP] : sz[(jz + 2 * RZ) % RZ];
+        *(VQ *)(d + Q * vq) = c;
+        if (xtra) *(VQ *)(d + Q * (TX / 2)) = e;
+    };
+
     // prefetch pipeline PF rows deep: slot 0 is consumed next
     V pc[PF], ph[PF], zc[PF], zh[PF], f1[PF], f2[PF];
+    VQ rc[PF], re[PF];
 #pragma unroll
-    for (int k = 0; k < PF; ++k) pc[k] = ph[k] = zc[k] = zh[k] = f1[k] = f2[k] = V{0, 0};
+    for (int k = 0; k < PF; ++k) {
+        pc[k] = ph[k] = zc[k] = zh[k] = f1[k] = f2[k] = V{0, 0};
+        rc[k] = re[k] = VQ{};
+    }
     auto fetch_psi = [&](int j, V &c, V &h) {
         const T *r = rowp(psi, prs, j);
         load_pair(r, c);
@@ -553,7 +582,17 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
 
     // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 into LDS, every load issued
     // before the first LDS write (see tendency_kernel)
-    {
+    if constexpr (R16) {
+        VQ q0c[5], q0e[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            q0c[k] = q0e[k] = VQ{};
+            if (is_psi || k < 3) fetch16(jb0 - 2 + k, jb0 - 1 + k, q0c[k], q0e[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            if (is_psi || k < 3) commit16(jb0 - 2 + k, jb0 - 1 + k, q0c[k], q0e[k]);
+    } else {
         V p0c[5], p0h[5], z0c[3], z0h[3];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -574,8 +613,12 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
     for (int k = 0; k < PF; ++k) {
         const int j = jb0 + k;
         if (j + 2 <= jb1) {
-            fetch_psi(j + 3, pc[k], ph[k]);
-            fetch_zeta(j + 2, zc[k], zh[k]);
+            if constexpr (R16) {
+                fetch16(j + 3, j + 2, rc[k], re[k]);
+            } else {
+                fetch_psi(j + 3, pc[k], ph[k]);
+                fetch_zeta(j + 2, zc[k], zh[k]);
+            }
         }
         if (j < jb1) fetch_f(j, f1[k], f2[k]);
     }
@@ -590,8 +633,12 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
     for (int j = jb0; j < jb1; ++j) {
         const bool more = j + 2 <= jb1;
         if (more) {
-            commit(sp[ring(j + 3, RP)], pc[0], ph[0]);
-            commit(sz[ring(j + 2, RZ)], zc[0], zh[0]);
+            if constexpr (R16) {
+                commit16(j + 3, j + 2, rc[0], re[0]);
+            } else {
+                commit(sp[ring(j + 3, RP)], pc[0], ph[0]);
+                commit(sz[ring(j + 2, RZ)], zc[0], zh[0]);
+            }
         }
         const V f1c = f1[0], f2c = f2[0];
         asm volatile("" : : "v"(f1c), "v"(f2c) : "memory");  // (see tendency_kernel)
@@ -601,14 +648,20 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
             ph[k] = ph[k + 1];
             zc[k] = zc[k + 1];
             zh[k] = zh[k + 1];
+            rc[k] = rc[k + 1];
+            re[k] = re[k + 1];
             f1[k] = f1[k + 1];
             f2[k] = f2[k + 1];
         }
         {
             const int jn = j + PF;  // iteration whose inputs are fetched now
             if (jn + 2 <= jb1) {
-                fetch_psi(jn + 3, pc[PF - 1], ph[PF - 1]);
-                fetch_zeta(jn + 2, zc[PF - 1], zh[PF - 1]);
+                if constexpr (R16) {
+                    fetch16(jn + 3, jn + 2, rc[PF - 1], re[PF - 1]);
+                } else {
+                    fetch_psi(jn + 3, pc[PF - 1], ph[PF - 1]);
+                    fetch_zeta(jn + 2, zc[PF - 1], zh[PF - 1]);
+                }
             }
             if (jn < jb1) fetch_f(jn, f1[PF - 1], f2[PF - 1]);
         }
