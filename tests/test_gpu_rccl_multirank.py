@@ -1,0 +1,127 @@
+"""Multi-rank RCCL on the one GPU of the test box.  RCCL refuses two ranks on one device of one
+host ("Duplicate GPU detected"), so each rank process here declares a host of its own
+(NCCL_HOSTID) and the ranks talk through RCCL's network transport over loopback
+(NCCL_SOCKET_IFNAME=lo).  What runs is the library's real multi-rank RCCL code -- grouped
+ncclSend/ncclRecv to two DISTINCT peers for the halo rows, ncclAllGather of the solver records
+over 2 and 4 ranks, the PCG dot-product gathers, the watchdog waits -- not the host transport
+and not the one-rank ring.  The transport between the ranks is loopback TCP, so nothing here
+measures xGMI; the slabs must reproduce the single-GPU run of the same global model exactly as
+the host-transport slabs do (tests/test_gpu_multirank.py)."""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def rccl_rank_env(rank):
+    """Environment of one RCCL rank sharing the GPU with others: its own host id (RCCL's
+    duplicate-GPU check compares host and bus id), the network transport over loopback."""
+    return {"NCCL_HOSTID": f"qg-rehearsal-rank{rank}", "NCCL_SOCKET_IFNAME": "lo",
+            "NCCL_IB_DISABLE": "1", "NCCL_NET": "Socket"}
+
+
+def _worker(rank, world, port, M, P, steps, outdir, solver, overlap):
+    import sys
+
+    os.environ.update(rccl_rank_env(rank))  # (before RCCL is loaded)
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # (uid broadcast, barriers)
+    torch.cuda.set_device(0)
+    import ctypes as C
+
+    import qgamd
+
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        buf = C.create_string_buffer(128)
+        qgamd._lib.call("qg_comm_unique_id", buf)
+        uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
+    dist.broadcast(uid, 0)
+    m = qgamd.bench_model(M, P=P)
+    st = qgamd.State(m, P_local=P // world, solver=solver)
+    st.comm_init(world, rank, bytes(uid.numpy().tobytes()))
+    st.set_overlap(overlap)
+    st.initialise()
+    st.run(1, steps)
+    torch.cuda.synchronize()
+    np.savez(os.path.join(outdir, f"rank{rank}.npz"), **{n: st.to_numpy(n) for n in ("zeta", "psi", "f_store")})
+    dist.barrier()
+    del st
+    dist.destroy_process_group()
+
+
+def _run(world, M, P, steps, d, solver, overlap):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:  # (a rank left waiting in a collective: stop exactly these children)
+        if p.exitcode is None:
+            p.terminate()
+            p.join(timeout=30)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("world,M,P,steps,solver,overlap",
+                         [(2, 64, 64, 6, 0, True), (2, 64, 64, 6, 0, False), (4, 64, 64, 5, 0, True),
+                          (2, 64, 64, 5, 1, True), (2, 1024, 128, 4, 0, True)])
+def test_rccl_slabs_match_single_gpu(world, M, P, steps, solver, overlap):
+    """solver 0 = spectral (halo send/recv + record all-gather), 1 = PCG with the spectral
+    preconditioner (its dot-product gathers and z halo also cross RCCL)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+
+    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps, solver=solver)
+    torch.cuda.synchronize()
+    g = {n: ref.to_numpy(n) for n in ("zeta", "psi", "f_store")}
+    with tempfile.TemporaryDirectory() as d:
+        loc = _run(world, M, P, steps, d, solver, overlap)
+    Pl = P // world
+    for r in range(world):
+        for n in ("zeta", "psi", "f_store"):
+            want = g[n][:, r * Pl: r * Pl + Pl + 2]
+            err = np.linalg.norm(loc[r][n] - want) / np.linalg.norm(want)
+            assert err < 1e-12, (r, n, err)
+
+
+def test_rccl_overlap_is_bit_identical():
+    """The halo exchange on the second stream while the interior rows run, over real multi-rank
+    RCCL: every slot of both slabs bit for bit equal to the serial schedule."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with tempfile.TemporaryDirectory() as d0, tempfile.TemporaryDirectory() as d1:
+        a = _run(2, 64, 64, 6, d0, 0, False)
+        b = _run(2, 64, 64, 6, d1, 0, True)
+    for r in range(2):
+        for n in ("zeta", "psi", "f_store"):
+            assert np.array_equal(a[r][n], b[r][n]), (r, n)
