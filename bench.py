@@ -78,6 +78,12 @@ def parse():
                     help="N > 1: RCCL over xGMI (default), or the host transport over gloo -- a "
                          "rehearsal of the multi-rank bench with several ranks on one GPU (slow, "
                          "not a measurement)")
+    ap.add_argument("--one-gpu", action="store_true",
+                    help="N > 1 over RCCL with every rank on GPU 0: each rank declares a host of its own "
+                         "to RCCL (NCCL_HOSTID; RCCL refuses two ranks on one device of one host), so "
+                         "RCCL's network transport over loopback carries the halo send/recv and the "
+                         "all-gathers -- a rehearsal of the multi-GPU code path on a one-GPU box (not "
+                         "xGMI, not a measurement)")
     ap.add_argument("--overlap", dest="overlap", action="store_true", default=True,
                     help="N > 1 (or --comm-self): post the halo exchange on a second stream while the "
                          "interior rows' tendency runs (qg_set_overlap; bit-identical results; the default)")
@@ -242,6 +248,13 @@ def validate_record(out):
     return True
 
 
+def rccl_one_gpu_env(rank):
+    """Environment of one RCCL rank sharing a GPU with other ranks (--one-gpu): its own host
+    id for RCCL's duplicate-GPU check, the socket transport over loopback."""
+    return {"NCCL_HOSTID": f"qg-rehearsal-rank{rank}", "NCCL_SOCKET_IFNAME": "lo",
+            "NCCL_IB_DISABLE": "1", "NCCL_NET": "Socket"}
+
+
 def _free_port():
     import socket
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
@@ -300,6 +313,9 @@ def main():
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     if args.graph:
         os.environ["QG_GRAPH"] = "1"
+    one_gpu = args.one_gpu and args.gpus > 1 and args.transport == "rccl"
+    if one_gpu:  # (before RCCL initialises)
+        os.environ.update(rccl_one_gpu_env(int(os.environ.get("RANK", "0"))))
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -307,7 +323,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU")
-    torch.cuda.set_device(local if args.transport == "rccl" else local % max(1, torch.cuda.device_count()))
+    dev = 0 if one_gpu else (local if args.transport == "rccl" else local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -315,7 +332,7 @@ def main():
         if args.transport == "host":
             dist.init_process_group("gloo")
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
 
     import qgamd
 
@@ -539,7 +556,9 @@ def main():
             "solver": ("spectral (x-DFT + parallel cyclic tridiagonal in y, direct)" if args.solver == "spectral"
                        else "matrix-free PCG on the 5-point operator, spectral preconditioner"),
             "finite": finite,
-            "transport": (args.transport if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
+            "transport": (("rccl, all ranks on one GPU: network transport over loopback (--one-gpu rehearsal, "
+                           "not xGMI, not a measurement)" if one_gpu else args.transport)
+                          if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
             "halo_overlap": bool(args.overlap and (world > 1 or args.comm_self)),
         },
         "roofline": {

@@ -27,18 +27,13 @@ def _free_port():
     return p
 
 
-def rccl_rank_env(rank):
-    """Environment of one RCCL rank sharing the GPU with others: its own host id (RCCL's
-    duplicate-GPU check compares host and bus id), the network transport over loopback."""
-    return {"NCCL_HOSTID": f"qg-rehearsal-rank{rank}", "NCCL_SOCKET_IFNAME": "lo",
-            "NCCL_IB_DISABLE": "1", "NCCL_NET": "Socket"}
-
-
 def _worker(rank, world, port, M, P, steps, outdir, solver, overlap):
     import sys
 
-    os.environ.update(rccl_rank_env(rank))  # (before RCCL is loaded)
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+    from bench import rccl_one_gpu_env
+
+    os.environ.update(rccl_one_gpu_env(rank))  # (before RCCL initialises)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -125,3 +120,89 @@ def test_rccl_overlap_is_bit_identical():
     for r in range(2):
         for n in ("zeta", "psi", "f_store"):
             assert np.array_equal(a[r][n], b[r][n]), (r, n)
+
+
+# ---- BASELINE configs 4 and 5 at their workload size over multi-rank RCCL ----------------
+
+def _config_worker(rank, world, port, M, steps, outdir, f32):
+    """One slab of an M x (world*M) model over RCCL; saves its current zeta and psi slots
+    (both layers, ghost rows included) for the parent's comparison with one GPU."""
+    import sys
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+    from bench import rccl_one_gpu_env
+
+    os.environ.update(rccl_one_gpu_env(rank))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import ctypes as C
+
+    import qgamd
+
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        buf = C.create_string_buffer(128)
+        qgamd._lib.call("qg_comm_unique_id", buf)
+        uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
+    dist.broadcast(uid, 0)
+    m = qgamd.bench_model(M, P=world * M, dt=60.0)
+    st = qgamd.State(m, P_local=M, dtype=torch.float32 if f32 else torch.float64)
+    st.comm_init(world, rank, bytes(uid.numpy().tobytes()))
+    st.initialise()
+    st.run(1, steps)
+    st.synchronize()  # (collective: the lazily refreshed ghost rows)
+    for n in ("zeta", "psi"):
+        np.save(os.path.join(outdir, f"{n}{rank}.npy"), getattr(st, n)[st.slot(n, 1)].cpu().numpy())
+    dist.barrier()
+    del st
+    dist.destroy_process_group()
+
+
+# bars: test_gpu_configs.py's (F32 psi: the white-noise field's rounding amplified by the
+# gravest Poisson modes, DESIGN 4)
+@pytest.mark.parametrize("world,M,steps,f32,tol", [(4, 4096, 4, False, {"zeta": 1e-10, "psi": 1e-10}),
+                                                   (8, 8192, 3, True, {"zeta": 1e-6, "psi": 1e-2})])
+def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, capsys):
+    """config 4: four 4096^2 F64 slabs (global 4096 x 16384); config 5: eight 8192^2 F32 slabs
+    (global 8192 x 65536) -- over multi-rank RCCL, against the single-GPU run of the global
+    model (the same bars as the host-transport form in test_gpu_configs.py)."""
+    import torch
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_config_worker, args=(r, world, port, M, steps, d, f32)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=400)
+        for p in procs:
+            if p.exitcode is None:
+                p.terminate()
+                p.join(timeout=30)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        m = qgamd.bench_model(M, P=world * M, dt=60.0)
+        glob = qgamd.State(m, dtype=torch.float32 if f32 else torch.float64)
+        glob.initialise()
+        glob.run(1, steps)
+        torch.cuda.synchronize()
+        worst = {}
+        for r in range(world):
+            for n in ("zeta", "psi"):
+                g = getattr(glob, n)[glob.slot(n, 1)][:, r * M: r * M + M + 2].double()
+                a = torch.from_numpy(np.load(os.path.join(d, f"{n}{r}.npy"))).cuda().double()
+                e = float(torch.linalg.vector_norm((a - g).reshape(-1)) / torch.linalg.vector_norm(g.reshape(-1)))
+                worst[n] = max(worst.get(n, 0.0), e)
+    with capsys.disabled():
+        print(f"\nRCCL {world} x {M}^2 {'F32' if f32 else 'F64'} slabs vs one GPU, {steps} steps: {worst}")
+    assert all(worst[n] < tol[n] for n in worst), worst
