@@ -212,7 +212,12 @@ int qg_diagnostics(qg_ctx *ctx, qg_diag *out);
  * ring neighbours and all-gathers one small record per rank (the spectral solver's
  * cross-slab carries); both go through the transport set up here.                       */
 int qg_comm_unique_id(char out[128]);               /* ncclGetUniqueId on rank 0          */
-int qg_comm_init(qg_ctx *ctx, int nranks, int rank, const char id[128]);  /* RCCL          */
+/* RCCL.  Collective over the nranks ranks (ncclCommInitRank, then one ring exchange and one
+ * all-gather at a small and a large size, so every peer connection the stepping uses exists
+ * before the first step: afterwards a peer that stops answering leaves only RCCL kernels
+ * waiting on the device, which the bounded waits below abort, never this host thread inside
+ * RCCL's lazy connection handshake).                                                     */
+int qg_comm_init(qg_ctx *ctx, int nranks, int rank, const char id[128]);
 /* Host-provided transport (MPI, tests, ...).  Both callbacks receive DEVICE pointers and the
  * stream the library works on; they must complete the transfer in stream order (e.g.
  * synchronise the stream, copy, exchange, copy back) and return 0 on success.

@@ -61,6 +61,37 @@ static int comm_setup_watchdog(Comm *c) {
     return QG_OK;
 }
 
+static int post(Comm *c, double *const xbuf[4], int64_t cnt, hipStream_t s);
+
+// RCCL connects peers lazily, inside the host call of the first operation that needs them
+// (ncclGroupEnd / ncclAllGather), in a handshake with the peer.  A peer that died before its
+// first exchange would then hold this rank's host thread inside RCCL, where no watchdog runs
+// (measured over the loopback network transport: rank 0 blocked in its first exchange for as
+// long as its peer stayed silent).  So comm_init, which every rank calls together, runs one
+// ring exchange and one all-gather at a small and a large message size: every connection the
+// stepping uses is made while all ranks are known to be alive, and afterwards a silent peer
+// only leaves RCCL kernels waiting on the device, which the bounded waits abort.
+static int comm_warmup(Comm *c) {
+    constexpr int64_t W = 131072;  // doubles: 1 MB, above every protocol's size threshold
+    hipStream_t s = nullptr;
+    double *buf = nullptr;
+    QG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int st = QG_OK;
+    if (hipMalloc((void **)&buf, sizeof(double) * (size_t)(4 + c->nranks) * W) != hipSuccess) st = QG_ERR_HIP;
+    if (st == QG_OK) (void)hipMemsetAsync(buf, 0, sizeof(double) * (size_t)(4 + c->nranks) * W, s);
+    for (int64_t n : {(int64_t)512, W}) {
+        if (st != QG_OK) break;
+        double *xbuf[4] = {buf, buf + W, buf + 2 * W, buf + 3 * W};
+        st = post(c, xbuf, n, s);
+        if (st == QG_OK && ncclAllGather(buf, buf + 4 * W, (size_t)n, ncclDouble, c->nccl, s) != ncclSuccess)
+            st = QG_ERR_RCCL;
+    }
+    if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_init (connection warm-up)");
+    if (buf) (void)hipFree(buf);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
 int comm_init(void **comm, int nranks, int rank, const char id[128]) {
     Comm *c = new Comm();
     c->nranks = nranks;
@@ -78,6 +109,15 @@ int comm_init(void **comm, int nranks, int rank, const char id[128]) {
             delete c;
             return QG_ERR_RCCL;
         }
+    }
+    const int w = comm_warmup(c);
+    if (w != QG_OK) {
+        std::fprintf(stderr, "qg_mi355 rank %d/%d: RCCL connection warm-up failed\n", rank, nranks);
+        if (c->nccl) ncclCommAbort(c->nccl);
+        c->nccl = nullptr;
+        if (c->progress_h) (void)hipHostFree(c->progress_h);
+        delete c;
+        return w;
     }
     *comm = c;
     return QG_OK;

@@ -206,3 +206,141 @@ def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, capsys):
     with capsys.disabled():
         print(f"\nRCCL {world} x {M}^2 {'F32' if f32 else 'F64'} slabs vs one GPU, {steps} steps: {worst}")
     assert all(worst[n] < tol[n] for n in worst), worst
+
+
+# ---- failure paths over multi-rank RCCL -------------------------------------------------
+
+def _rccl_state(rank, world, port, m, **kw):
+    """(torch, dist, qgamd, State over RCCL) in a rank process (see _worker)."""
+    import sys
+
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
+    from bench import rccl_one_gpu_env
+
+    os.environ.update(rccl_one_gpu_env(rank))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    import ctypes as C
+
+    import qgamd
+
+    uid = torch.zeros(128, dtype=torch.uint8)
+    if rank == 0:
+        buf = C.create_string_buffer(128)
+        qgamd._lib.call("qg_comm_unique_id", buf)
+        uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
+    dist.broadcast(uid, 0)
+    st = qgamd.State(m(qgamd), P_local=kw.pop("P_local"), **kw)
+    st.comm_init(world, rank, bytes(uid.numpy().tobytes()))
+    return torch, dist, qgamd, st
+
+
+def _silent_peer_worker(rank, world, port, outdir):
+    """rank 1 joins the communicator and then never steps; rank 0 must get QG_ERR_RCCL from its
+    watchdog (ncclCommAbort), not hang in the halo exchange."""
+    import ctypes as C
+    import json
+    import time
+
+    torch, dist, qgamd, st = _rccl_state(rank, world, port, lambda q: q.bench_model(64, P=64), P_local=32)
+    st.initialise()
+    dist.barrier()
+    if rank == 1:
+        time.sleep(25)
+        os._exit(0)  # (its communicator's peer has aborted: no orderly destroy)
+    qgamd._lib.call("qg_comm_set_timeout", st._ctx, C.c_double(2.0))
+    t0 = time.perf_counter()
+    res = {"status": 0}
+    try:
+        st.run(1, 64)
+        st.synchronize()
+    except qgamd.QGError as e:
+        res["status"] = e.status
+    res["waited"] = time.perf_counter() - t0
+    open(os.path.join(outdir, "silent.json"), "w").write(json.dumps(res))
+    os._exit(0)
+
+
+def test_rccl_silent_peer_returns_rccl_error():
+    import json
+
+    import torch
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from qgamd import _lib
+
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_silent_peer_worker, args=(r, 2, port, d)) for r in range(2)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=120)
+        for p in procs:
+            if p.exitcode is None:
+                p.terminate()
+                p.join(timeout=30)
+        res = json.load(open(os.path.join(d, "silent.json")))
+    assert res["status"] == _lib.QG_ERR_RCCL, res
+    assert res["waited"] < 20, res  # the watchdog's 2 s (plus the abort), not the peer's 25 s
+
+
+def _cert_fail_rccl_worker(rank, world, port, outdir):
+    import json
+
+    torch, dist, qgamd, st = _rccl_state(rank, world, port, lambda q: q.bench_model(64, P=64), P_local=64 // world,
+                                         solver=1, pcg_rtol=1e-30)
+    st.initialise()
+    res = {"stop": -1}
+    for t in range(1, 200):  # the reference's loop, one call per step
+        st.evolve_zeta_(t)
+        try:
+            st.evolve_psi_()
+        except qgamd.QGError as e:
+            res["status"] = e.status
+            res["stop"] = t
+            break
+    res["cert"] = st.pcg_certificate()
+    open(os.path.join(outdir, f"cert{rank}.json"), "w").write(json.dumps(res))
+    dist.barrier()
+    del st
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_failed_certificate_stops_every_rank_at_the_same_step(world):
+    """Deferred PCG with an unreachable residual target across RCCL slabs: every rank reports
+    QG_ERR_NOT_CONVERGED at the same step (the latch poll is collective), none steps on into an
+    exchange its peers never post."""
+    import json
+
+    import torch
+    import torch.multiprocessing as mp
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with tempfile.TemporaryDirectory() as d:
+        ctx = mp.get_context("spawn")
+        port = _free_port()
+        procs = [ctx.Process(target=_cert_fail_rccl_worker, args=(r, world, port, d)) for r in range(world)]
+        for p in procs:
+            p.start()
+        for p in procs:
+            p.join(timeout=240)
+        for p in procs:
+            if p.exitcode is None:
+                p.terminate()
+                p.join(timeout=30)
+        assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+        res = [json.load(open(os.path.join(d, f"cert{r}.json"))) for r in range(world)]
+    assert all(r.get("status") == -7 for r in res), res
+    assert len({r["stop"] for r in res}) == 1 and 16 <= res[0]["stop"] <= 3 * 16 + 1, res
+    assert len({json.dumps(r["cert"], sort_keys=True) for r in res}) == 1, res
