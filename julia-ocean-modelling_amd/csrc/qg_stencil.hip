@@ -117,8 +117,18 @@ __device__ __forceinline__ TendBlock tend_block() {
 // P_fwd^-1 psi, A_s psi~ = sum_l P_fwd^-1[s][l] (lap(psi_l) + alpha_s psi_l) (lap(psi_l) is
 // the ring's own), summed over the two layers through LDS; (b,b), (r,r) per workgroup.
 // One strip (see tendency_pair_strip for EDGE: false = the x-halo inside the row, so no
-// periodic wraps and no ghost-column stores in the row loop).
-template <int TX, int PF, class T, bool CERT, bool EDGE>
+// periodic wraps and no ghost-column stores in the row loop).  IN_ROWS: every row the strip
+// reads (jb0-2 .. jb1+1) is a local row and no output row is a ghost-row image (2 <= jb0,
+// jb1 + 2 <= P): the row pointers then advance by ld per row, with no range checks.
+//
+// Scalar work per row.  The loop's addressing is wave-uniform, so it runs on the CU's one
+// scalar ALU, which all resident waves share: with ring slots as (j + 2R) % R per access (a
+// signed division by 6 / 5 / 4 each), row pointers as (j + 1) * ld products and the kernel
+// arguments re-read after the asm barrier below, the 4096^2 F64 tendency issued 2.1 scalar
+// instructions per vector one -- 1.36e8 per launch, 529 k per CU in 809 k cycles
+// (SQ_INSTS_SALU, r04k).  Now the ring slots are pointer arrays rotated once per row, the row
+// pointers induction variables, and the arguments read once.
+template <int TX, int PF, class T, bool CERT, bool EDGE, bool IN_ROWS>
 __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer, int t, int x0, int jb0, int jb1,
                                                T (*sp)[TX + 4], T (*sz)[TX + 2], T (*sl)[TX + 2],
                                                double (*xch)[4][CERT ? TX : 1]) {
@@ -151,6 +161,12 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
     const T *zeta = a.zeta[layer];
     const RowSrcT<T> &prs = a.psi_rows[layer];
     const RowSrcT<T> &zrs = a.zeta_rows[layer];
+    // the arguments the row loop uses, read once
+    const T *const fp1 = a.fprev1[layer], *const fp2 = a.fprev2[layer];
+    T *const zo = a.zeta_out[layer], *const fo = a.f_out[layer];
+    T *const fs1 = a.fshift1[layer], *const fs2 = a.fshift2[layer];
+    const double *const wind = layer == 0 ? a.wind : nullptr;  // wind extension (off: nullptr)
+    const bool gr = a.write_ghost_rows != 0;
     // model constants in the state's precision (the same expressions as the F64 path)
     const T dx = (T)a.dx, idx = T(1) / dx, idx2 = idx * idx;
     const T cdc = T(0.5) * idx;
@@ -164,7 +180,7 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
         return x < 0 ? x + M : (x >= M ? x - M : x);
     };
     auto rowp = [&](const T *base, const RowSrcT<T> &rs, int j) -> const T * {
-        if (j >= 0 && j < P) return base + fidx(1, j + 1, ld);
+        if (IN_ROWS || (j >= 0 && j < P)) return base + fidx(1, j + 1, ld);
         return rs.halo[j < 0 ? j + 2 : (j - P) + 2];
     };
     // per-thread column positions: psi LDS position t+2 (own) and the halo position
@@ -180,41 +196,47 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
     T pc[PF], ph[PF], zc[PF], zh[PF], f1[PF], f2[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) pc[k] = ph[k] = zc[k] = zh[k] = f1[k] = f2[k] = 0;
-    auto fetch_psi = [&](int j, T &c, T &h) {
-        const T *r = rowp(psi, prs, j);
+    auto fetch_psi = [&](const T *r, T &c, T &h) {  // r: interior element 0 of the row
         c = r[xo];
         if (ph_q >= 0) h = r[xph];
     };
-    auto fetch_zeta = [&](int j, T &c, T &h) {
-        const T *r = rowp(zeta, zrs, j);
+    auto fetch_zeta = [&](const T *r, T &c, T &h) {
         c = r[xo];
         if (zh_q >= 0) h = r[xzh];
     };
-    auto fetch_f = [&](int j, T &g1, T &g2) {
+    auto fetch_f = [&](size_t o, T &g1, T &g2) {  // o: element offset of the row's interior element 0
         if (ab3 && has_out) {
-            const size_t o = (size_t)(j + 1) * ld;  // uniform row offset
-            g1 = ld_stream(a.fprev1[layer] + o + i + 1);
-            g2 = ld_stream(a.fprev2[layer] + o + i + 1);
+            g1 = ld_stream(fp1 + o + i);
+            g2 = ld_stream(fp2 + o + i);
         }
     };
-    auto commit_psi = [&](int j, T c, T h) {
-        T *d = sp[(j + 2 * RP) % RP];
+    auto commit_psi = [&](auto d, T c, T h) {
         d[t + 2] = c;
         if (ph_q >= 0) d[ph_q] = h;
     };
-    auto commit_zeta = [&](int j, T c, T h) {
-        T *d = sz[(j + 2 * RZ) % RZ];
+    auto commit_zeta = [&](auto d, T c, T h) {
         d[t + 1] = c;
         if (zh_q >= 0) d[zh_q] = h;
     };
-    auto lap_row = [&](int j) {  // lap(psi) at row j, LDS positions 0..TX+1 (x0-1 .. x0+TX)
-        const T *pm = sp[(j - 1 + 2 * RP) % RP], *p0 = sp[(j + 2 * RP) % RP], *pp = sp[(j + 1 + 2 * RP) % RP];
-        T *dst = sl[(j + 2 * RL) % RL];
+    // lap(psi) of the row whose psi rows below / at / above are pm, p0, pp: LDS positions
+    // 0..TX+1 (x0-1 .. x0+TX)
+    auto lap_row = [&](auto pm, auto p0, auto pp, auto dst) {
         for (int q = t; q < TX + 2; q += TX) {
             const int c = q + 1;
             dst[q] = ((((p0[c - 1] + p0[c + 1]) - T(4) * p0[c]) + pm[c]) + pp[c]) * idx2;
         }
     };
+    // ring slots of the rows the iteration j uses: rP[k] = psi row j-2+k, rZ[k] = zeta row
+    // j-1+k, rL[k] = lap row j-1+k; rotated by one at the end of every row
+    // (LDS-typed: 32-bit addresses, one scalar register per slot)
+    typedef __attribute__((address_space(3))) T *LT;
+    LT rP[RP], rZ[RZ], rL[RL];
+#pragma unroll
+    for (int k = 0; k < RP; ++k) rP[k] = (LT)sp[(jb0 - 2 + k + 2 * RP) % RP];
+#pragma unroll
+    for (int k = 0; k < RZ; ++k) rZ[k] = (LT)sz[(jb0 - 1 + k + 2 * RZ) % RZ];
+#pragma unroll
+    for (int k = 0; k < RL; ++k) rL[k] = (LT)sl[(jb0 - 1 + k + 2 * RL) % RL];
 
     // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 into LDS.  All eight rows' loads
     // are issued before the first LDS write (a fetch-commit loop waited one full memory latency
@@ -225,17 +247,17 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             p0c[k] = p0h[k] = 0;
-            fetch_psi(jb0 - 2 + k, p0c[k], p0h[k]);
+            fetch_psi(rowp(psi, prs, jb0 - 2 + k), p0c[k], p0h[k]);
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             z0c[k] = z0h[k] = 0;
-            fetch_zeta(jb0 - 1 + k, z0c[k], z0h[k]);
+            fetch_zeta(rowp(zeta, zrs, jb0 - 1 + k), z0c[k], z0h[k]);
         }
 #pragma unroll
-        for (int k = 0; k < 5; ++k) commit_psi(jb0 - 2 + k, p0c[k], p0h[k]);
+        for (int k = 0; k < 5; ++k) commit_psi(rP[k], p0c[k], p0h[k]);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) commit_zeta(jb0 - 1 + k, z0c[k], z0h[k]);
+        for (int k = 0; k < 3; ++k) commit_zeta(rZ[k], z0c[k], z0h[k]);
     }
     // prefetch for iterations jb0 .. jb0+PF-1: psi row j+3, zeta row j+2 (committed while
     // rows are still needed, i.e. j+2 <= jb1) and F of row j
@@ -243,22 +265,27 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
     for (int k = 0; k < PF; ++k) {
         const int j = jb0 + k;
         if (j + 2 <= jb1) {
-            fetch_psi(j + 3, pc[k], ph[k]);
-            fetch_zeta(j + 2, zc[k], zh[k]);
+            fetch_psi(rowp(psi, prs, j + 3), pc[k], ph[k]);
+            fetch_zeta(rowp(zeta, zrs, j + 2), zc[k], zh[k]);
         }
-        if (j < jb1) fetch_f(j, f1[k], f2[k]);
+        if (j < jb1) fetch_f((size_t)(j + 1) * ld + 1, f1[k], f2[k]);
     }
     __syncthreads();
-    lap_row(jb0 - 1);
-    lap_row(jb0);
-    lap_row(jb0 + 1);
+    lap_row(rP[0], rP[1], rP[2], rL[0]);
+    lap_row(rP[1], rP[2], rP[3], rL[1]);
+    lap_row(rP[2], rP[3], rP[4], rL[2]);
+
+    // IN_ROWS row pointers: the next fetch (iteration j + PF) and this row's outputs
+    const T *nP = psi + fidx(1, jb0 + PF + 3 + 1, ld), *nZ = zeta + fidx(1, jb0 + PF + 2 + 1, ld);
+    size_t nF = (size_t)(jb0 + PF + 1) * ld + 1;
+    size_t oRow = (size_t)(jb0 + 1) * ld;
 
     const T bl = (T)a.beta[layer];
     for (int j = jb0; j < jb1; ++j) {
         const bool more = j + 2 <= jb1;  // psi row j+3 / zeta row j+2 / lap row j+2 needed
         if (more) {
-            commit_psi(j + 3, pc[0], ph[0]);
-            commit_zeta(j + 2, zc[0], zh[0]);
+            commit_psi(rP[5], pc[0], ph[0]);
+            commit_zeta(rZ[3], zc[0], zh[0]);
         }
         const T f1c = f1[0], f2c = f2[0];
         // land this row's F(t-1), F(t-2) (issued last iteration) before the next row's loads
@@ -277,30 +304,30 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
         {
             const int jn = j + PF;  // iteration whose inputs are fetched now
             if (jn + 2 <= jb1) {
-                fetch_psi(jn + 3, pc[PF - 1], ph[PF - 1]);
-                fetch_zeta(jn + 2, zc[PF - 1], zh[PF - 1]);
+                fetch_psi(IN_ROWS ? nP : rowp(psi, prs, jn + 3), pc[PF - 1], ph[PF - 1]);
+                fetch_zeta(IN_ROWS ? nZ : rowp(zeta, zrs, jn + 2), zc[PF - 1], zh[PF - 1]);
             }
-            if (jn < jb1) fetch_f(jn, f1[PF - 1], f2[PF - 1]);
+            if (jn < jb1) fetch_f(IN_ROWS ? nF : (size_t)(jn + 1) * ld + 1, f1[PF - 1], f2[PF - 1]);
         }
         __syncthreads();
         if constexpr (CERT) {
             if (layer == 0) cert_fold();  // row j-1: layer 1 wrote its part before this barrier
         }
-        if (more) lap_row(j + 2);
+        if (more) lap_row(rP[3], rP[4], rP[5], rL[3]);
         if (has_out) {
-            const T *Lm = sl[(j - 1 + 2 * RL) % RL], *L0 = sl[(j + 2 * RL) % RL], *Lp = sl[(j + 1 + 2 * RL) % RL];
-            const T *Pm = sp[(j - 1 + 2 * RP) % RP], *P0 = sp[(j + 2 * RP) % RP], *Pp = sp[(j + 1 + 2 * RP) % RP];
-            const T *Zm = sz[(j - 1 + 2 * RZ) % RZ], *Z0 = sz[(j + 2 * RZ) % RZ], *Zp = sz[(j + 1 + 2 * RZ) % RZ];
+            const LT Lm = rL[0], L0 = rL[1], Lp = rL[2];
+            const LT Pm = rP[1], P0 = rP[2], Pp = rP[3];
+            const LT Zm = rZ[0], Z0 = rZ[1], Zp = rZ[2];
             const int cl = t + 1;  // centre in sl / sz (x-halo 1)
             const int cp = t + 2;  // centre in sp (x-halo 2)
             const T biharm = ((((L0[cl - 1] + L0[cl + 1]) - T(4) * L0[cl]) + Lm[cl]) + Lp[cl]) * idx2;
             const T v_term = visc * biharm;
             auto Z = [&](int da, int db) {
-                const T *r = db < 0 ? Zm : (db > 0 ? Zp : Z0);
+                const LT r = db < 0 ? Zm : (db > 0 ? Zp : Z0);
                 return r[cl + da];
             };
             auto S = [&](int da, int db) {
-                const T *r = db < 0 ? Pm : (db > 0 ? Pp : P0);
+                const LT r = db < 0 ? Pm : (db > 0 ? Pp : P0);
                 return r[cp + da];
             };
             const T J_term = arakawa_point<T>(Z, S, den);
@@ -309,18 +336,16 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
             if (layer == 0) last = Ut * (cdc * (Z0[cl + 1] - Z0[cl - 1]));  // U * cd(zeta)
             else last = rt * L0[cl];                                         // r * lap(psi)
             T F = ((v_term - J_term) - beta_term) - last;
-            if (layer == 0 && a.wind) F = F + (T)a.wind[j];  // wind extension (off: nullptr)
+            if (wind) F = F + (T)wind[j];
             const T zcen = Z0[cl];
             const T zn = ab3 ? zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * f1c)) + ((T)(5.0 / 12.0) * f2c))
                              : zcen + (dtT * F);
-            T *zo = a.zeta_out[layer], *fo = a.f_out[layer];
-            const bool gr = a.write_ghost_rows;
-            store_row_with_ghosts<T, EDGE>(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, i, zn);
-            store_row_with_ghosts<T, EDGE>(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, i, F);
-            if (ab3 && a.fshift1[layer]) {  // (see TendArgsT::fshift1)
-                T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
-                store_row_with_ghosts<T, EDGE>(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, i, f1c);
-                store_row_with_ghosts<T, EDGE>(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, i, f2c);
+            const size_t orow = IN_ROWS ? oRow : (size_t)(j + 1) * ld;
+            store_row_with_ghosts<T, EDGE>(zo + orow, IN_ROWS ? nullptr : ghost_row_target(zo, ld, P, j, gr), M, i, zn);
+            store_row_with_ghosts<T, EDGE>(fo + orow, IN_ROWS ? nullptr : ghost_row_target(fo, ld, P, j, gr), M, i, F);
+            if (ab3 && fs1) {  // (see TendArgsT::fshift1)
+                store_row_with_ghosts<T, EDGE>(fs1 + orow, IN_ROWS ? nullptr : ghost_row_target(fs1, ld, P, j, gr), M, i, f1c);
+                store_row_with_ghosts<T, EDGE>(fs2 + orow, IN_ROWS ? nullptr : ghost_row_target(fs2, ld, P, j, gr), M, i, f2c);
             }
             if constexpr (CERT) {  // this layer's parts of b_s and r_s at (i, j)
                 double part[4];
@@ -340,6 +365,23 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
                 }
             }
         }
+        // the next row: ring slots rotate by one, row pointers advance by one row
+        {
+            const LT p0 = rP[0], z0 = rZ[0], l0 = rL[0];
+#pragma unroll
+            for (int k = 0; k + 1 < RP; ++k) rP[k] = rP[k + 1];
+#pragma unroll
+            for (int k = 0; k + 1 < RZ; ++k) rZ[k] = rZ[k + 1];
+#pragma unroll
+            for (int k = 0; k + 1 < RL; ++k) rL[k] = rL[k + 1];
+            rP[RP - 1] = p0;
+            rZ[RZ - 1] = z0;
+            rL[RL - 1] = l0;
+        }
+        nP += ld;
+        nZ += ld;
+        nF += ld;
+        oRow += ld;
     }
     if constexpr (CERT) {
         __syncthreads();
@@ -364,7 +406,7 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
 }
 
 template <int TX, int PF, class T, bool CERT = false>
-__global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
+__global__ __launch_bounds__(CERT ? 2 * TX : TX, (CERT || TX >= 512) ? 4 : 5) void tendency_kernel(TendArgsT<T> a, int nyA, int nyB) {
     constexpr int RP = 6, RZ = 5, RL = 4;  // ring depths
     constexpr int NL = CERT ? 2 : 1;       // layers per workgroup
     const TendBlock tb = tend_block();
@@ -394,10 +436,13 @@ __global__ __launch_bounds__(CERT ? 2 * TX : TX) void tendency_kernel(TendArgsT<
     // barrier (double-buffered by row parity); layer 0 keeps its own for that row meanwhile
     __shared__ double xch[CERT ? 2 : 1][4][CERT ? TX : 1];
     const int L = CERT ? layer : 0;
-    if (x0 >= 2 && x0 + TX + 2 <= M)  // (uniform) the x-halo inside the row
-        tendency_strip<TX, PF, T, CERT, false>(a, layer, t, x0, jb0, jb1, sp_[L], sz_[L], sl_[L], xch);
-    else
-        tendency_strip<TX, PF, T, CERT, true>(a, layer, t, x0, jb0, jb1, sp_[L], sz_[L], sl_[L], xch);
+    const bool in_rows = jb0 >= 2 && jb1 + 2 <= (int)a.P;  // (uniform) see tendency_strip
+    if (x0 >= 2 && x0 + TX + 2 <= M) {  // (uniform) the x-halo inside the row
+        if (in_rows) tendency_strip<TX, PF, T, CERT, false, true>(a, layer, t, x0, jb0, jb1, sp_[L], sz_[L], sl_[L], xch);
+        else tendency_strip<TX, PF, T, CERT, false, false>(a, layer, t, x0, jb0, jb1, sp_[L], sz_[L], sl_[L], xch);
+    } else {
+        tendency_strip<TX, PF, T, CERT, true, false>(a, layer, t, x0, jb0, jb1, sp_[L], sz_[L], sl_[L], xch);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -451,7 +496,9 @@ __device__ __forceinline__ void store_pair_with_ghosts(T *row, T *grow, int M, i
 // all but the first and the last): no periodic wrap of column indices, every pair in range,
 // no ghost-column stores -- the interior strips' row loop is straight-line code except for
 // the halo lanes.  EDGE = true: the general form (wraps, partial pairs, ghost columns).
-template <int TX, class T, int PF, bool EDGE>
+// IN_ROWS and the scalar bookkeeping (rotated ring slots, induction row pointers, arguments
+// read once): see tendency_strip.
+template <int TX, class T, int PF, bool EDGE, bool IN_ROWS>
 __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int layer, int x0, int jb0, int jb1,
                                                     T (*sp)[2 * TX + 4], T (*sz)[2 * TX + 4], T (*sl)[2 * TX + 4]) {
     using V = typename PairT<T>::V;
@@ -466,6 +513,12 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
     const T *zeta = a.zeta[layer];
     const RowSrcT<T> &prs = a.psi_rows[layer];
     const RowSrcT<T> &zrs = a.zeta_rows[layer];
+    // the arguments the row loop uses, read once
+    const T *const fp1 = a.fprev1[layer], *const fp2 = a.fprev2[layer];
+    T *const zo = a.zeta_out[layer], *const fo = a.f_out[layer];
+    T *const fs1 = a.fshift1[layer], *const fs2 = a.fshift2[layer];
+    const double *const wind = layer == 0 ? a.wind : nullptr;  // wind extension (off: nullptr)
+    const bool gr = a.write_ghost_rows != 0;
     const T dx = (T)a.dx, idx = T(1) / dx, idx2 = idx * idx;
     const T cdc = T(0.5) * idx;
     const T den = T(12) * (dx * dx);
@@ -478,7 +531,7 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
         return x < 0 ? x + M : (x >= M ? x - M : x);
     };
     auto rowp = [&](const T *base, const RowSrcT<T> &rs, int j) -> const T * {
-        if (j >= 0 && j < P) return base + fidx(1, j + 1, ld);
+        if (IN_ROWS || (j >= 0 && j < P)) return base + fidx(1, j + 1, ld);
         return rs.halo[j < 0 ? j + 2 : (j - P) + 2];
     };
     const int hq = t == 0 ? 0 : (t == TX - 1 ? W + 2 : -1);  // halo pair LDS index, or none
@@ -503,6 +556,16 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
             h = V{v.x, v.y};
         }
     };
+    // ring slots of the rows the iteration j uses (LDS-typed: 32-bit addresses): rP[k] = psi
+    // row j-2+k, rZ[k] = zeta row j-1+k, rL[k] = lap row j-1+k; rotated by one every row
+    typedef __attribute__((address_space(3))) T *LT;
+    LT rP[RP], rZ[RZ], rL[RL];
+#pragma unroll
+    for (int k = 0; k < RP; ++k) rP[k] = (LT)sp[(jb0 - 2 + k + 2 * RP) % RP];
+#pragma unroll
+    for (int k = 0; k < RZ; ++k) rZ[k] = (LT)sz[(jb0 - 1 + k + 2 * RZ) % RZ];
+#pragma unroll
+    for (int k = 0; k < RL; ++k) rL[k] = (LT)sl[(jb0 - 1 + k + 2 * RL) % RL];
     // Ring rows of interior strips 16 B per lane: threads [0, TX/2) read the psi row, [TX/2, TX)
     // the zeta row, each as (W + 4) / Q vectors of Q elements (x0-2 .. x0+W+1); threads 0 and
     // TX/2 take the one vector left over each.  One 16-byte load and LDS store per lane and row
@@ -517,15 +580,15 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
     const bool is_psi = t < TX / 2;  // (wave-uniform for TX % 128 == 0)
     const int vq = is_psi ? t : t - TX / 2;
     const bool xtra = t == 0 || t == TX / 2;  // vector TX/2 of its row
-    auto fetch16 = [&](int jp, int jz, VQ &c, VQ &e) {
-        const T *r = (is_psi ? rowp(psi, prs, jp) : rowp(zeta, zrs, jz)) + (x0 - 2);
+    auto fetch16 = [&](const T *rp, const T *rz, VQ &c, VQ &e) {  // (rows' interior element 0)
+        const T *r = (is_psi ? rp : rz) + (x0 - 2);
         c = *(const VQU *)(r + Q * vq);
         if (xtra) e = *(const VQU *)(r + Q * (TX / 2));
     };
-    auto commit16 = [&](int jp, int jz, VQ c, VQ e) {
-        T *d = is_psi ? sp[(jp + 2 * RP) % RP] : sz[(jz + 2 * RZ) % RZ];
-        *(VQ *)(d + Q * vq) = c;
-        if (xtra) *(VQ *)(d + Q * (TX / 2)) = e;
+    auto commit16 = [&](LT dp, LT dz, VQ c, VQ e) {
+        const LT d = is_psi ? dp : dz;
+        *(__attribute__((address_space(3))) VQ *)(d + Q * vq) = c;
+        if (xtra) *(__attribute__((address_space(3))) VQ *)(d + Q * (TX / 2)) = e;
     };
 
     // prefetch pipeline PF rows deep: slot 0 is consumed next
@@ -536,20 +599,13 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
         pc[k] = ph[k] = zc[k] = zh[k] = f1[k] = f2[k] = V{0, 0};
         rc[k] = re[k] = VQ{};
     }
-    auto fetch_psi = [&](int j, V &c, V &h) {
-        const T *r = rowp(psi, prs, j);
+    auto fetch_pair_row = [&](const T *r, V &c, V &h) {
         load_pair(r, c);
         load_halo(r, h);
     };
-    auto fetch_zeta = [&](int j, V &c, V &h) {
-        const T *r = rowp(zeta, zrs, j);
-        load_pair(r, c);
-        load_halo(r, h);
-    };
-    auto fetch_f = [&](int j, V &g1, V &g2) {
+    auto fetch_f = [&](size_t o, V &g1, V &g2) {  // o: element offset of the row's interior element 0
         if (ab3 && has_a) {
-            const size_t o = (size_t)(j + 1) * ld + 1;
-            const T *p1 = a.fprev1[layer] + o, *p2 = a.fprev2[layer] + o;
+            const T *p1 = fp1 + o, *p2 = fp2 + o;
             if (has_b) {
                 const VU u1 = *(const VU *)(p1 + xa), u2 = *(const VU *)(p2 + xa);
                 g1 = V{u1.x, u1.y};
@@ -560,21 +616,18 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
             }
         }
     };
-    auto commit = [&](T *d, V c, V h) {
-        *(V *)(d + c0) = c;
-        if (hq >= 0) *(V *)(d + hq) = h;
+    auto commit = [&](LT d, V c, V h) {
+        *(__attribute__((address_space(3))) V *)(d + c0) = c;
+        if (hq >= 0) *(__attribute__((address_space(3))) V *)(d + hq) = h;
     };
-    auto ring = [](int j, int R) { return (j + 2 * R) % R; };
-    auto lap_row = [&](int j) {  // lap(psi) at x0-1 .. x0+W (LDS 1 .. W+2)
-        const T *pm = sp[ring(j - 1, RP)], *p0 = sp[ring(j, RP)], *pp = sp[ring(j + 1, RP)];
-        T *dst = sl[ring(j, RL)];
-        const V a0 = *(const V *)(p0 + c0 - 2), a1 = *(const V *)(p0 + c0),
-                    a2 = *(const V *)(p0 + c0 + 2);
-        const V m = *(const V *)(pm + c0), p = *(const V *)(pp + c0);
+    auto lap_row = [&](LT pm, LT p0, LT pp, LT dst) {  // lap(psi) at x0-1 .. x0+W (LDS 1 .. W+2)
+        typedef __attribute__((address_space(3))) V *LV;
+        const V a0 = *(LV)(p0 + c0 - 2), a1 = *(LV)(p0 + c0), a2 = *(LV)(p0 + c0 + 2);
+        const V m = *(LV)(pm + c0), p = *(LV)(pp + c0);
         V r;
         r.x = ((((a0.y + a1.y) - T(4) * a1.x) + m.x) + p.x) * idx2;
         r.y = ((((a1.x + a2.x) - T(4) * a1.y) + m.y) + p.y) * idx2;
-        *(V *)(dst + c0) = r;
+        *(LV)(dst + c0) = r;
         if (t == 0) dst[1] = ((((p0[0] + p0[2]) - T(4) * p0[1]) + pm[1]) + pp[1]) * idx2;
         if (t == TX - 1)
             dst[W + 2] = ((((p0[W + 1] + p0[W + 3]) - T(4) * p0[W + 2]) + pm[W + 2]) + pp[W + 2]) * idx2;
@@ -587,57 +640,60 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             q0c[k] = q0e[k] = VQ{};
-            if (is_psi || k < 3) fetch16(jb0 - 2 + k, jb0 - 1 + k, q0c[k], q0e[k]);
+            if (is_psi || k < 3) fetch16(rowp(psi, prs, jb0 - 2 + k), rowp(zeta, zrs, jb0 - 1 + k), q0c[k], q0e[k]);
         }
 #pragma unroll
         for (int k = 0; k < 5; ++k)
-            if (is_psi || k < 3) commit16(jb0 - 2 + k, jb0 - 1 + k, q0c[k], q0e[k]);
+            if (is_psi || k < 3) commit16(rP[k], rZ[k], q0c[k], q0e[k]);
     } else {
         V p0c[5], p0h[5], z0c[3], z0h[3];
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
             p0c[k] = p0h[k] = V{0, 0};
-            fetch_psi(jb0 - 2 + k, p0c[k], p0h[k]);
+            fetch_pair_row(rowp(psi, prs, jb0 - 2 + k), p0c[k], p0h[k]);
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
             z0c[k] = z0h[k] = V{0, 0};
-            fetch_zeta(jb0 - 1 + k, z0c[k], z0h[k]);
+            fetch_pair_row(rowp(zeta, zrs, jb0 - 1 + k), z0c[k], z0h[k]);
         }
 #pragma unroll
-        for (int k = 0; k < 5; ++k) commit(sp[ring(jb0 - 2 + k, RP)], p0c[k], p0h[k]);
+        for (int k = 0; k < 5; ++k) commit(rP[k], p0c[k], p0h[k]);
 #pragma unroll
-        for (int k = 0; k < 3; ++k) commit(sz[ring(jb0 - 1 + k, RZ)], z0c[k], z0h[k]);
+        for (int k = 0; k < 3; ++k) commit(rZ[k], z0c[k], z0h[k]);
     }
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
         const int j = jb0 + k;
         if (j + 2 <= jb1) {
             if constexpr (R16) {
-                fetch16(j + 3, j + 2, rc[k], re[k]);
+                fetch16(rowp(psi, prs, j + 3), rowp(zeta, zrs, j + 2), rc[k], re[k]);
             } else {
-                fetch_psi(j + 3, pc[k], ph[k]);
-                fetch_zeta(j + 2, zc[k], zh[k]);
+                fetch_pair_row(rowp(psi, prs, j + 3), pc[k], ph[k]);
+                fetch_pair_row(rowp(zeta, zrs, j + 2), zc[k], zh[k]);
             }
         }
-        if (j < jb1) fetch_f(j, f1[k], f2[k]);
+        if (j < jb1) fetch_f((size_t)(j + 1) * ld + 1, f1[k], f2[k]);
     }
     __syncthreads();
-    lap_row(jb0 - 1);
-    lap_row(jb0);
-    lap_row(jb0 + 1);
+    lap_row(rP[0], rP[1], rP[2], rL[0]);
+    lap_row(rP[1], rP[2], rP[3], rL[1]);
+    lap_row(rP[2], rP[3], rP[4], rL[2]);
+
+    // IN_ROWS row pointers: the next fetch (iteration j + PF) and this row's outputs
+    const T *nP = psi + fidx(1, jb0 + PF + 3 + 1, ld), *nZ = zeta + fidx(1, jb0 + PF + 2 + 1, ld);
+    size_t nF = (size_t)(jb0 + PF + 1) * ld + 1;
+    size_t oRow = (size_t)(jb0 + 1) * ld;
 
     const T bl = (T)a.beta[layer];
-    T *zo = a.zeta_out[layer], *fo = a.f_out[layer];
-    const bool gr = a.write_ghost_rows;
     for (int j = jb0; j < jb1; ++j) {
         const bool more = j + 2 <= jb1;
         if (more) {
             if constexpr (R16) {
-                commit16(j + 3, j + 2, rc[0], re[0]);
+                commit16(rP[5], rZ[3], rc[0], re[0]);
             } else {
-                commit(sp[ring(j + 3, RP)], pc[0], ph[0]);
-                commit(sz[ring(j + 2, RZ)], zc[0], zh[0]);
+                commit(rP[5], pc[0], ph[0]);
+                commit(rZ[3], zc[0], zh[0]);
             }
         }
         const V f1c = f1[0], f2c = f2[0];
@@ -656,39 +712,38 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
         {
             const int jn = j + PF;  // iteration whose inputs are fetched now
             if (jn + 2 <= jb1) {
+                const T *rp = IN_ROWS ? nP : rowp(psi, prs, jn + 3), *rz = IN_ROWS ? nZ : rowp(zeta, zrs, jn + 2);
                 if constexpr (R16) {
-                    fetch16(jn + 3, jn + 2, rc[PF - 1], re[PF - 1]);
+                    fetch16(rp, rz, rc[PF - 1], re[PF - 1]);
                 } else {
-                    fetch_psi(jn + 3, pc[PF - 1], ph[PF - 1]);
-                    fetch_zeta(jn + 2, zc[PF - 1], zh[PF - 1]);
+                    fetch_pair_row(rp, pc[PF - 1], ph[PF - 1]);
+                    fetch_pair_row(rz, zc[PF - 1], zh[PF - 1]);
                 }
             }
-            if (jn < jb1) fetch_f(jn, f1[PF - 1], f2[PF - 1]);
+            if (jn < jb1) fetch_f(IN_ROWS ? nF : (size_t)(jn + 1) * ld + 1, f1[PF - 1], f2[PF - 1]);
         }
         __syncthreads();
-        if (more) lap_row(j + 2);
+        if (more) lap_row(rP[3], rP[4], rP[5], rL[3]);
         if (has_a) {
+            typedef __attribute__((address_space(3))) V *LV;
             // 4-wide windows (LDS c0-1 .. c0+2) of the zeta / psi rows j-1, j, j+1 and lap row j;
             // lap rows j-1, j+1 at the pair only
             T Zw[3][4], Sw[3][4], L0w[4];
-            const T *zr[3] = {sz[ring(j - 1, RZ)], sz[ring(j, RZ)], sz[ring(j + 1, RZ)]};
-            const T *pr[3] = {sp[ring(j - 1, RP)], sp[ring(j, RP)], sp[ring(j + 1, RP)]};
+            const LT zr[3] = {rZ[0], rZ[1], rZ[2]};
+            const LT pr[3] = {rP[1], rP[2], rP[3]};
 #pragma unroll
             for (int r = 0; r < 3; ++r) {
-                const V u0 = *(const V *)(zr[r] + c0 - 2), u1 = *(const V *)(zr[r] + c0),
-                            u2 = *(const V *)(zr[r] + c0 + 2);
+                const V u0 = *(LV)(zr[r] + c0 - 2), u1 = *(LV)(zr[r] + c0), u2 = *(LV)(zr[r] + c0 + 2);
                 Zw[r][0] = u0.y; Zw[r][1] = u1.x; Zw[r][2] = u1.y; Zw[r][3] = u2.x;
-                const V s0 = *(const V *)(pr[r] + c0 - 2), s1 = *(const V *)(pr[r] + c0),
-                            s2 = *(const V *)(pr[r] + c0 + 2);
+                const V s0 = *(LV)(pr[r] + c0 - 2), s1 = *(LV)(pr[r] + c0), s2 = *(LV)(pr[r] + c0 + 2);
                 Sw[r][0] = s0.y; Sw[r][1] = s1.x; Sw[r][2] = s1.y; Sw[r][3] = s2.x;
             }
-            const T *l0 = sl[ring(j, RL)];
+            const LT l0 = rL[1];
             {
-                const V u0 = *(const V *)(l0 + c0 - 2), u1 = *(const V *)(l0 + c0),
-                            u2 = *(const V *)(l0 + c0 + 2);
+                const V u0 = *(LV)(l0 + c0 - 2), u1 = *(LV)(l0 + c0), u2 = *(LV)(l0 + c0 + 2);
                 L0w[0] = u0.y; L0w[1] = u1.x; L0w[2] = u1.y; L0w[3] = u2.x;
             }
-            const V Lm = *(const V *)(sl[ring(j - 1, RL)] + c0), Lp = *(const V *)(sl[ring(j + 1, RL)] + c0);
+            const V Lm = *(LV)(rL[0] + c0), Lp = *(LV)(rL[2] + c0);
             T out_z[2], out_f[2];
 #pragma unroll
             for (int v = 0; v < 2; ++v) {
@@ -704,25 +759,42 @@ __device__ __forceinline__ void tendency_pair_strip(const TendArgsT<T> &a, int l
                 if (layer == 0) last = Ut * (cdc * (Zw[1][w + 1] - Zw[1][w - 1]));
                 else last = rt * L0w[w];
                 T F = ((v_term - J_term) - beta_term) - last;
-                if (layer == 0 && a.wind) F = F + (T)a.wind[j];  // wind extension (off: nullptr)
+                if (wind) F = F + (T)wind[j];
                 const T zcen = Zw[1][w];
                 const T g1 = v ? f1c.y : f1c.x, g2 = v ? f2c.y : f2c.x;
                 out_z[v] = ab3 ? zcen + dtT * ((((T)(23.0 / 12.0) * F) - ((T)(16.0 / 12.0) * g1)) + ((T)(5.0 / 12.0) * g2))
                                : zcen + (dtT * F);
                 out_f[v] = F;
             }
-            store_pair_with_ghosts<T, EDGE>(zo + (size_t)(j + 1) * ld, ghost_row_target(zo, ld, P, j, gr), M, xa,
+            const size_t orow = IN_ROWS ? oRow : (size_t)(j + 1) * ld;
+            store_pair_with_ghosts<T, EDGE>(zo + orow, IN_ROWS ? nullptr : ghost_row_target(zo, ld, P, j, gr), M, xa,
                                             out_z[0], out_z[1], has_b);
-            store_pair_with_ghosts<T, EDGE>(fo + (size_t)(j + 1) * ld, ghost_row_target(fo, ld, P, j, gr), M, xa,
+            store_pair_with_ghosts<T, EDGE>(fo + orow, IN_ROWS ? nullptr : ghost_row_target(fo, ld, P, j, gr), M, xa,
                                             out_f[0], out_f[1], has_b);
-            if (ab3 && a.fshift1[layer]) {  // (see TendArgsT::fshift1)
-                T *s1 = a.fshift1[layer], *s2 = a.fshift2[layer];
-                store_pair_with_ghosts<T, EDGE>(s1 + (size_t)(j + 1) * ld, ghost_row_target(s1, ld, P, j, gr), M, xa,
-                                                f1c.x, f1c.y, has_b);
-                store_pair_with_ghosts<T, EDGE>(s2 + (size_t)(j + 1) * ld, ghost_row_target(s2, ld, P, j, gr), M, xa,
-                                                f2c.x, f2c.y, has_b);
+            if (ab3 && fs1) {  // (see TendArgsT::fshift1)
+                store_pair_with_ghosts<T, EDGE>(fs1 + orow, IN_ROWS ? nullptr : ghost_row_target(fs1, ld, P, j, gr), M,
+                                                xa, f1c.x, f1c.y, has_b);
+                store_pair_with_ghosts<T, EDGE>(fs2 + orow, IN_ROWS ? nullptr : ghost_row_target(fs2, ld, P, j, gr), M,
+                                                xa, f2c.x, f2c.y, has_b);
             }
         }
+        // the next row: ring slots rotate by one, row pointers advance by one row
+        {
+            const LT p0 = rP[0], z0 = rZ[0], l0 = rL[0];
+#pragma unroll
+            for (int k = 0; k + 1 < RP; ++k) rP[k] = rP[k + 1];
+#pragma unroll
+            for (int k = 0; k + 1 < RZ; ++k) rZ[k] = rZ[k + 1];
+#pragma unroll
+            for (int k = 0; k + 1 < RL; ++k) rL[k] = rL[k + 1];
+            rP[RP - 1] = p0;
+            rZ[RZ - 1] = z0;
+            rL[RL - 1] = l0;
+        }
+        nP += ld;
+        nZ += ld;
+        nF += ld;
+        oRow += ld;
     }
 }
 
@@ -743,10 +815,13 @@ __global__ __launch_bounds__(TX) void tendency_pair_kernel(TendArgsT<T> a, int n
     __shared__ __attribute__((aligned(16))) T sp[RP][WL];
     __shared__ __attribute__((aligned(16))) T sz[RZ][WL];
     __shared__ __attribute__((aligned(16))) T sl[RL][WL];
-    if (x0 >= 2 && x0 + W + 2 <= M)  // (uniform) the x-halo inside the row
-        tendency_pair_strip<TX, T, PF, false>(a, tb.z, x0, jb0, jb1, sp, sz, sl);
-    else
-        tendency_pair_strip<TX, T, PF, true>(a, tb.z, x0, jb0, jb1, sp, sz, sl);
+    const bool in_rows = jb0 >= 2 && jb1 + 2 <= (int)a.P;  // (uniform) see tendency_strip
+    if (x0 >= 2 && x0 + W + 2 <= M) {  // (uniform) the x-halo inside the row
+        if (in_rows) tendency_pair_strip<TX, T, PF, false, true>(a, tb.z, x0, jb0, jb1, sp, sz, sl);
+        else tendency_pair_strip<TX, T, PF, false, false>(a, tb.z, x0, jb0, jb1, sp, sz, sl);
+    } else {
+        tendency_pair_strip<TX, T, PF, true, false>(a, tb.z, x0, jb0, jb1, sp, sz, sl);
+    }
 }
 
 // ------------------------------------------------------------------------------------
