@@ -178,11 +178,14 @@ def pcg_variant(qgamd, m, n, warmup, K, torch, warm_ms=300.0):
                     "step's tendency, verdict latched there -- no host round trip)"}
 
 
-def dropin_variant(qgamd, m, n, warmup, K, torch):
+def dropin_variant(qgamd, m, n, warmup, K, torch, slot1=False):
     """The drop-in path: the reference's loop body on bare (M+2, P+2, 2, 3) device arrays,
     evolve_zeta!(model, zeta, psi, t, f_store) then evolve_psi!(model, zeta, psi, P, H)
     (model.jl:155, :172), each call leaving slot 1 = newest as store_new_state! does (the
-    history shifted in place on the device).  K timed steps after the warm-up."""
+    history shifted in place on the device).  K timed steps after the warm-up.  slot1:
+    set_dropin_slots("slot1") -- slots 2-3 of zeta and psi, which the reference never reads,
+    not maintained (QG_KEEP_ORDER_SLOT1)."""
+    qgamd.set_dropin_slots("slot1" if slot1 else "all")
     src = qgamd.State(m, P_local=n)
     src.initialise()
     zeta, psi, f_store = src.zeta, src.psi, src.f_store  # (heads 0 after initialise)
@@ -202,11 +205,15 @@ def dropin_variant(qgamd, m, n, warmup, K, torch):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     qgamd.unbind(zeta, psi, f_store)
+    qgamd.set_dropin_slots("all")
     del src
-    return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K,
-            "note": "reference array signatures from Python (ctypes per call), slot order kept on every "
-                    "call by an in-place history shift (store_new_state!'s 2 slot copies per field; "
-                    "f_store's done by the AB3 tendency as it reads F(t-1), F(t-2))"}
+    note = ("reference array signatures from Python (ctypes per call), slot order kept on every "
+            "call by an in-place history shift (store_new_state!'s 2 slot copies per field; "
+            "f_store's done by the AB3 tendency as it reads F(t-1), F(t-2))")
+    if slot1:
+        note = ("as dropin, with slots 2-3 of zeta and psi (never read by the reference) not maintained: "
+                "the new zeta written to slot 2 and copied to slot 1, psi solved into slot 1, f_store as dropin")
+    return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K, "note": note}
 
 
 # the JSON line's contract (the driver's fields + this bench's sub-records); checked before
@@ -591,12 +598,13 @@ def main():
             and not args.comm_self:
         del st
         torch.cuda.empty_cache()
-        try:
-            d = dropin_variant(qgamd, m, n, 3, args.dropin_steps, torch)
-            d["vs_qg_run_step"] = d["ms_per_step"] / ms
-        except Exception as e:  # noqa: BLE001 -- reported, the headline line is still printed
-            d = {"error": f"{type(e).__name__}: {e}"}
-        out["dropin"] = d
+        for key, slot1 in (("dropin", False), ("dropin_slot1", True)):
+            try:
+                d = dropin_variant(qgamd, m, n, 3, args.dropin_steps, torch, slot1=slot1)
+                d["vs_qg_run_step"] = d["ms_per_step"] / ms
+            except Exception as e:  # noqa: BLE001 -- reported, the headline line is still printed
+                d = {"error": f"{type(e).__name__}: {e}"}
+            out[key] = d
     if args.cpu_steps > 0 and world == 1 and args.dtype == "f64":
         out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads, args.cpu_steps_1t)
     else:

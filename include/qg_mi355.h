@@ -153,7 +153,13 @@ int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2
  * history itself as it reads it (each slot rewritten with its periodic ghost images).
  * on = 1 canonicalizes first.  For callers that
  * hand the reference's arrays to every call (evolve_zeta!(model, zeta, psi, t, f_store));
- * qg_run is faster rotating (the default, on = 0).                                          */
+ * qg_run is faster rotating (the default, on = 0).
+ * on = QG_KEEP_ORDER_SLOT1 (2): slot 1 of zeta and psi and all three slots of f_store as
+ * above after every call, slots 2-3 of zeta and psi NOT maintained -- the reference never
+ * reads them (only evolve_zeta_layer! reads f_store's history), so its loop computes the
+ * same values: no shifts of zeta and psi, the new zeta written to slot 2 and copied to slot 1
+ * (one slot copy per step instead of four).                                                  */
+#define QG_KEEP_ORDER_SLOT1 2
 int qg_set_keep_order(qg_ctx *ctx, int on);
 int qg_get_stats(qg_ctx *ctx, qg_stats *out);
 /* PCG with the spectral preconditioner and an invertible P_fwd (the default) takes the

@@ -86,8 +86,10 @@ struct qg_ctx {
     int64_t pace_count = 0;
     // qg_set_keep_order: every call leaves slot 1 = newest, as store_new_state! does
     // (model.jl:102-106), by shifting the history slots in place before the new values are
-    // written; the heads then stay 0
-    bool keep_order = false;
+    // written; the heads then stay 0.  QG_KEEP_ORDER_SLOT1 (lean): slots 2-3 of zeta and psi,
+    // which the reference never reads, are not maintained (no shifts of zeta and psi; the new
+    // zeta goes through slot 2, one slot copy)
+    int keep_order = 0;
     bool no_fshift_fuse = std::getenv("QG_NO_FSHIFT_FUSE") != nullptr;  // (A/B: the separate shift)
     bool capturing = false;  // a step graph is being captured (no host reads, no polls)
     // deferred PCG: the latch is copied to page-locked memory every QG_PACE_STEPS steps and
@@ -374,13 +376,24 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     // only zeta is shifted here -- zeta's slot 1 is read with a stencil and cannot be
     // overwritten in place
     const bool fuse_fshift = c->keep_order && !c->distributed && timestep >= 3 && !c->no_fshift_fuse;
-    if (c->keep_order) {
+    const bool lean = c->keep_order == QG_KEEP_ORDER_SLOT1;
+    if (c->keep_order && !lean) {
         void *arr[2] = {c->zeta, c->fst};
         QG_CHECK(launch_slot_shift(arr, fuse_fshift ? 1 : 2, 2 * c->esize * c->F, c->stream));
         zh = 1;
         fh = fuse_fshift ? 0 : 1;
         fh2 = fuse_fshift ? 1 : 2;
         zn = fn = 0;
+    } else if (lean) {  // zeta: read slot 1, new values to slot 2, copied to slot 1 below
+        if (!fuse_fshift) {
+            void *arr[1] = {c->fst};
+            QG_CHECK(launch_slot_shift(arr, 1, 2 * c->esize * c->F, c->stream));
+        }
+        zh = 0;
+        zn = 1;
+        fh = fuse_fshift ? 0 : 1;
+        fh2 = fuse_fshift ? 1 : 2;
+        fn = 0;
     }
     TendArgsT<T> a{};
     a.M = p.M;
@@ -476,6 +489,12 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
         }
         c->ghosts_pending = true;
     }
+    if (lean) {  // slot 1 <- slot 2 (ghost rows too; multi-rank: refreshed by the lazy flush)
+        static const int mv[1][3] = {{1, -1, -1}};
+        void *arr[1] = {c->zeta};
+        QG_CHECK(launch_slot_move(arr, mv, 1, 2 * c->esize * c->F, c->stream));
+        zn = 0;
+    }
     c->heads[0] = zn;
     c->heads[2] = fn;
     return QG_OK;
@@ -544,9 +563,11 @@ int qg_evolve_psi(qg_ctx *c) {
     QG_HIP(hipSetDevice(c->device));
     const int zh = c->heads[0];
     int pn = (c->heads[1] + 2) % 3;
-    if (c->keep_order) {  // store_new_state!'s shift of psi, then the solve writes slot 1
-        void *arr[1] = {c->psi};
-        QG_CHECK(launch_slot_shift(arr, 1, 2 * c->esize * c->F, c->stream));
+    if (c->keep_order) {  // store_new_state!'s shift of psi (lean: none), then the solve writes slot 1
+        if (c->keep_order != QG_KEEP_ORDER_SLOT1) {
+            void *arr[1] = {c->psi};
+            QG_CHECK(launch_slot_shift(arr, 1, 2 * c->esize * c->F, c->stream));
+        }
         pn = 0;
     }
     double *o1 = c->field(c->psi, 0, pn), *o2 = c->field(c->psi, 1, pn);  // (element type p.dtype)
@@ -697,10 +718,10 @@ int qg_canonicalize(qg_ctx *c) {
 }
 
 int qg_set_keep_order(qg_ctx *c, int on) {
-    if (!c) return QG_ERR_INVALID_ARG;
+    if (!c || on < 0 || on > QG_KEEP_ORDER_SLOT1) return QG_ERR_INVALID_ARG;
     if (on && !c->keep_order && c->zeta) QG_CHECK(qg_canonicalize(c));
-    if (c->keep_order != (on != 0)) drop_graphs(c);
-    c->keep_order = on != 0;
+    if (c->keep_order != on) drop_graphs(c);
+    c->keep_order = on;
     return QG_OK;
 }
 

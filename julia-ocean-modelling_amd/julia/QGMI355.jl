@@ -152,6 +152,19 @@ evolve_psi!(model, s::QGState, poisson=nothing, helmholtz=nothing) =
 # slot copies per field, the reference's own data movement).  (The rotation-free fast path
 # is QGState / run_model_no_output.)
 const _BOUND = Dict{NTuple{3,UInt},QGState}()
+# slots maintained on arrays bound from now on: 1 = all (store_new_state! exactly), 2 =
+# QG_KEEP_ORDER_SLOT1 (slot 1 of zeta / psi and all of f_store: the values the reference's
+# loop reads; one slot copy per step instead of four)
+const _DROPIN_SLOTS = Ref{Cint}(1)
+
+"""`set_dropin_slots!(:all | :slot1)`: the slots the reference-signature calls maintain on
+arrays bound from now on (`:slot1` leaves slots 2-3 of `zeta` / `psi`, which the reference
+never reads, unmaintained)."""
+function set_dropin_slots!(mode::Symbol)
+    mode in (:all, :slot1) || throw(ArgumentError("mode must be :all or :slot1"))
+    _DROPIN_SLOTS[] = mode === :slot1 ? Cint(2) : Cint(1)
+    mode
+end
 
 function _bound_state(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, f_store::ROCArray{T,4}) where {T}
     size(zeta) == size(psi) == size(f_store) == (model.M + 2, model.P + 2, 2, 3) ||
@@ -166,7 +179,7 @@ function _bound_state(model, zeta::ROCArray{T,4}, psi::ROCArray{T,4}, f_store::R
                              params, AMDGPU.device_id(AMDGPU.device()) - 1, stream_ptr(), ctx)
     @qgcheck qg_bind_state ccall((:qg_bind_state, libqg), Cint, (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}),
                                  ctx[], pointer(zeta), pointer(psi), pointer(f_store))
-    @qgcheck qg_set_keep_order ccall((:qg_set_keep_order, libqg), Cint, (Ptr{Cvoid}, Cint), ctx[], 1)
+    @qgcheck qg_set_keep_order ccall((:qg_set_keep_order, libqg), Cint, (Ptr{Cvoid}, Cint), ctx[], _DROPIN_SLOTS[])
     s = QGState{T}(ctx[], zeta, psi, f_store, model)
     finalizer(x -> ccall((:qg_destroy, libqg), Cint, (Ptr{Cvoid},), x.ctx), s)
     _BOUND[key] = s

@@ -10,13 +10,14 @@ from .model import *  # noqa: F401,F403
 from .model import (BaroclinicModel, PairSolver, State, bench_model, cd, device_zeros,
                     evolve_psi_, evolve_zeta_, get_helmholtz_cholesky, get_poisson_cholesky,
                     initialise_model, J, laplace_5p, make_model, run_model_no_output,
-                    sp_solve_modified_helmholtz, sp_solve_poisson, unbind, update_doubly_periodic_bc_)
+                    set_dropin_slots, sp_solve_modified_helmholtz, sp_solve_poisson, unbind,
+                    update_doubly_periodic_bc_)
 from .checkpoint import load_checkpoint, read_checkpoint, save_checkpoint
 from .run import SnapshotWriter, create_metadata, log_model_params, run_model, update_max, update_min
 
 __all__ = ["BaroclinicModel", "PairSolver", "State", "bench_model", "cd", "device_zeros",
            "evolve_psi_", "evolve_zeta_", "get_helmholtz_cholesky", "get_poisson_cholesky",
-           "initialise_model", "J", "laplace_5p", "make_model", "run_model_no_output",
+           "initialise_model", "J", "laplace_5p", "make_model", "run_model_no_output", "set_dropin_slots",
            "sp_solve_modified_helmholtz", "sp_solve_poisson", "unbind", "update_doubly_periodic_bc_",
            "run_model", "update_max", "update_min", "create_metadata", "log_model_params", "SnapshotWriter",
            "save_checkpoint", "load_checkpoint", "read_checkpoint", "LIB_PATH", "QGError", "lib"]

@@ -172,3 +172,72 @@ def test_reference_signatures_keep_order_and_unbind(qg, f32):
         qg.evolve_psi_(m2, zeta, psi, pc, hc)
     assert qg.unbind(zeta, psi, f_store) == 1
     assert qg.unbind(zeta, psi, f_store) == 0
+
+
+def _slot1_equal(b, a):
+    """b keeps QG_KEEP_ORDER_SLOT1 order: physical slot 0 of zeta / psi and every slot of
+    f_store equal (bitwise) to the rotating state a's logical ones."""
+    import torch
+    la = _logical(a)
+    assert torch.equal(b.zeta[0], la["zeta"][0]) and torch.equal(b.psi[0], la["psi"][0])
+    assert torch.equal(b.f_store, la["f_store"])
+
+
+# slot 1 only (slots 2-3 of zeta / psi unmaintained, never read by the reference): after every
+# evolve_zeta! the new zeta is in slot 1 (read back between the two calls), after every step
+# zeta, psi and f_store are what the rotating path holds -- both solvers, F32, the LDS-ring and
+# certifying tendencies (1280 x 1024), HIP-graph replay
+@pytest.mark.parametrize("M,P,solver,f32", [(64, 48, 0, False), (128, 128, 1, False), (64, 64, 0, True),
+                                            (1280, 1024, 0, False), (1280, 1024, 1, False), (1280, 1024, 0, True)])
+def test_keep_order_slot1_matches_rotation(qg, M, P, solver, f32):
+    import torch
+    m = qg.bench_model(M, P=P)
+    kw = dict(solver=solver, dtype=torch.float32 if f32 else None)
+    a = qg.initialise_model(m, **kw)
+    b = qg.initialise_model(m, **kw)
+    b.set_keep_order(True, slot1_only=True)
+    for t in range(1, 8):
+        a.evolve_zeta_(t)
+        b.evolve_zeta_(t)
+        assert torch.equal(b.zeta[0], a.logical("zeta")[0])  # slot 1 newest between the calls
+        a.evolve_psi_()
+        b.evolve_psi_()
+        assert b.heads() == [0, 0, 0]
+        _slot1_equal(b, a)
+    a.run(8, 11)
+    b.run(8, 11)
+    _slot1_equal(b, a)
+
+
+def test_keep_order_slot1_graph_replay(qg, monkeypatch):
+    m = qg.bench_model(128)
+    ref = qg.initialise_model(m, solver=1)
+    ref.run(1, 25)
+    monkeypatch.setenv("QG_GRAPH", "1")
+    st = qg.initialise_model(m, solver=1)
+    st.set_keep_order(True, slot1_only=True)
+    st.run(1, 25)
+    _slot1_equal(st, ref)
+
+
+def test_reference_signatures_slot1(qg):
+    """set_dropin_slots("slot1"): the reference-signature loop on bare arrays, slot 1 of zeta /
+    psi and all of f_store equal to the rotating State after every step."""
+    import torch
+    m = qg.bench_model(1280, P=1024)
+    ref = qg.initialise_model(m)
+    zeta, psi, f_store = ref.zeta.clone(), ref.psi.clone(), ref.f_store.clone()
+    pc = qg.get_poisson_cholesky(m.M, m.P, m.dx)
+    hc = qg.get_helmholtz_cholesky(m.M, m.P, m.dx, qg.S_eig(m))
+    qg.set_dropin_slots("slot1")
+    try:
+        for t in range(1, 7):
+            qg.evolve_zeta_(m, zeta, psi, t, f_store)
+            qg.evolve_psi_(m, zeta, psi, pc, hc)
+            ref.step(t)
+            la = _logical(ref)
+            assert torch.equal(zeta[0], la["zeta"][0]) and torch.equal(psi[0], la["psi"][0])
+            assert torch.equal(f_store, la["f_store"])
+    finally:
+        qg.set_dropin_slots("all")
+        qg.unbind(zeta, psi, f_store)
