@@ -237,6 +237,7 @@ __device__ __forceinline__ void tendency_strip(const TendArgsT<T> &a, int layer,
     for (int k = 0; k < RZ; ++k) rZ[k] = (LT)sz[(jb0 - 1 + k + 2 * RZ) % RZ];
 #pragma unroll
     for (int k = 0; k < RL; ++k) rL[k] = (LT)sl[(jb0 - 1 + k + 2 * RL) % RL];
+
     // prologue: psi rows jb0-2..jb0+2, zeta rows jb0-1..jb0+1 into LDS.  All eight rows' loads
     // are issued before the first LDS write (a fetch-commit loop waited one full memory latency
     // per row: eight round trips in front of every strip, while the workgroups of a chip-full,
