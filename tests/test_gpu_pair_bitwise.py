@@ -2,7 +2,8 @@
 default) against the one-point kernel it replaces (`tendency_kernel`, QG_TEND_PAIR=0): the
 same arithmetic in the same order per point, so every field must be bit-identical after
 several Euler + AB3 steps.  Grids above the direct kernel's cut-off (1.2 M points per layer)
-so the LDS-ring kernels run; M = 1500 leaves a partial last strip (F32 states need even M).  The kernel choice
+so the LDS-ring kernels run; M = 1500 leaves a partial last strip (F32 states need even M), the
+rows of whole strips run the 5-per-CU kernel, M = 1024 / 512 with every strip (one) an edge strip.  The kernel choice
 is read once per process, so each variant runs in its own child process."""
 import os
 import subprocess
@@ -24,7 +25,7 @@ np.savez(out, **{{n: st.to_numpy(n) for n in ("zeta", "psi", "f_store")}})
 """
 
 
-@pytest.mark.parametrize("M,P", [(2048, 1024), (1500, 1024)])
+@pytest.mark.parametrize("M,P", [(2048, 1024), (1500, 1024), (1024, 1536), (512, 4096)])
 def test_pair_kernel_bitwise_vs_one_point(M, P, tmp_path):
     import torch
     if not torch.cuda.is_available():
