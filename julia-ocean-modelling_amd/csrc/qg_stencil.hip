@@ -1148,8 +1148,11 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     // six chip-fulls from ~3500^2 up: with the batched ring prologue a strip's start costs one
     // memory latency, and shorter strips keep the chip's concurrent accesses closer together
     // (tools/waves_sweep.sh, profiles/r02/prologue: 4096^2 3 -> 6 chip-fulls 341.7 -> 335 us,
-    // 8192^2 4 -> 6 1 237-1 257 -> 1 230-1 241 us; before the prologue fix three and four)
-    const int waves = env_waves ? env_waves : (pts >= 12.0e6 ? 6 : (pts >= 3.0e6 ? 1 : 2));
+    // 8192^2 4 -> 6 1 237-1 257 -> 1 230-1 241 us; before the prologue fix three and four).
+    // Since the scalar-unit cuts (r04) a strip's start costs less and shorter walks pay:
+    // 4096^2 6 -> 9 chip-fulls 328 -> 323 us, 8192^2 12 -> 16 1 339 -> 1 317 us (6: 1 300 vs
+    // 12: 1 267 on another box; tools/r04_p.sh, profiles/r04/waves/)
+    const int waves = env_waves ? env_waves : (pts >= 40.0e6 ? 16 : (pts >= 12.0e6 ? 9 : (pts >= 3.0e6 ? 1 : 2)));
     const int target = std::max(1, waves * sl / (2 * nx));  // row workgroups per column strip
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -1243,11 +1246,12 @@ static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
     QG_CHECK(tend_slots(tendency_pair_kernel<TX, T, PF>, TX, sl));
     const char *e = std::getenv("QG_TEND_WAVES");
     const int nx = (int)((a.M + W - 1) / W);
-    // four chip-fulls at 8192^2 and up (tools/tend_waves_f32.sh: 797 -> 766 us)
     const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
     // (tools/sweep_r02g.sh with the batched prologue: 8192^2 4 -> 6 chip-fulls 773 -> 764 us;
-    // 4096^2 keeps 2: 209 vs 213-230 us)
-    const int waves = e ? std::max(1, std::atoi(e)) : (pts >= 40.0e6 ? 6 : 2);
+    // 4096^2 keeps 2: 209 vs 213-230 us.  r04, after the scalar-unit cuts: 8192^2 6 -> 12 -> 20
+    // chip-fulls 652-719 -> 613-670 -> 646-652 us (12 -> 20 on one box: 663-668 -> 646-652),
+    // tools/r04_p.sh, profiles/r04/waves/)
+    const int waves = e ? std::max(1, std::atoi(e)) : (pts >= 40.0e6 ? 20 : 2);
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
     const int target = std::max(1, waves * sl / (2 * nx));
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
