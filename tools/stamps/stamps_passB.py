@@ -1,4 +1,4 @@
-"""Phase timing of spec_passB<4096> from a stamp build (tools/exp: lib/exp/stampB.so, built from
+"""Phase timing of spec_passB<4096> from a stamp build (tools/stamps/add_stamps.py -> lib/exp/stampB.so, built from
 a copy of csrc with wall_clock64 stamps; not part of the product).  Prints per-phase medians."""
 import ctypes as C
 import os
