@@ -89,6 +89,10 @@ def parse():
                          "interior rows' tendency runs (qg_set_overlap; bit-identical results; the default)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="N > 1 (or --comm-self): the exchange in stream order before the whole tendency")
+    ap.add_argument("--halo", choices=["rccl", "peer"], default="rccl",
+                    help="RCCL transport: how the halo rows travel (qg_comm_set_halo_transport): rccl = "
+                         "pack + grouped send/recv; peer = copy-engine copies into the neighbours' "
+                         "IPC-mapped receive regions + arrival flags")
     ap.add_argument("--dropin-steps", type=int, default=20,
                     help="also time this many steps through the reference's own array signatures "
                          "(evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(...) on bare arrays, "
@@ -367,6 +371,8 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         st.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
+    if args.halo != "rccl" and args.transport == "rccl" and (world > 1 or args.comm_self):
+        st.set_halo_transport(args.halo)
     st.set_overlap(args.overlap)
     st.initialise()
     torch.cuda.synchronize()
@@ -567,6 +573,8 @@ def main():
                            "not xGMI, not a measurement)" if one_gpu else args.transport)
                           if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
             "halo_overlap": bool(args.overlap and (world > 1 or args.comm_self)),
+            "halo_transport": (getattr(st, "halo_transport", "rccl") if args.transport == "rccl"
+                               and (world > 1 or args.comm_self) else None),
         },
         "roofline": {
             "bound": "hbm",

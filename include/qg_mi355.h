@@ -257,6 +257,19 @@ int qg_comm_set_timeout(qg_ctx *ctx, double seconds);
  * same-process A/B runs (r04) -- the exchange completes inside the interior's tail.
  * No effect on a single GPU (no exchange) or for P < 8 (no interior worth splitting).   */
 int qg_set_overlap(qg_ctx *ctx, int on);
+/* How the halo rows of a step travel (RCCL transport only; collective: every rank calls it
+ * with the same value, after qg_comm_init).
+ * QG_HALO_RCCL (default): pack kernel + grouped ncclSend/ncclRecv.
+ * QG_HALO_PEER: each rank's receive region (uncached device memory) is opened by its ring
+ * neighbours through IPC; the rows are copied by the copy engine (hipMemcpyDeviceToDeviceNoCU)
+ * straight from the state into the neighbours' regions, a one-lane kernel raises their
+ * arrival flags and a one-lane kernel on the receiving side polls its own (bounded by the
+ * comm timeout; a missing peer then fails the transport with QG_ERR_RCCL).  No collective
+ * kernel holds compute units, so the exchange proceeds beside the interior tendency.
+ * QG_ERR_UNSUPPORTED (on every rank, the transport unchanged) when a rank cannot export or
+ * open the regions.  The environment variable QG_HALO_PEER=1 selects it in qg_comm_init. */
+enum { QG_HALO_RCCL = 0, QG_HALO_PEER = 1 };
+int qg_comm_set_halo_transport(qg_ctx *ctx, int transport);
 /* Time the two collectives of a multi-GPU step in isolation (HIP events on the context's
  * stream, `reps` back-to-back calls each; every rank calls it): out[0] = ms per halo exchange
  * (pack + grouped send/recv of the depth-2 rows of psi and zeta), out[1] = bytes this rank

@@ -23,6 +23,7 @@ int comm_halo_rows(void *comm, double *const *f2, int n2, int64_t ld, int64_t P,
 int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, double *const *f1, int n1, int64_t ld,
                   int64_t P, hipStream_t s, bool ghost_f2);
 int comm_init(void **comm, int nranks, int rank, const char id[128]);
+int comm_set_peer(void *comm, int on, int64_t ld);
 int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sendrecv_fn sr, void *user);
 int comm_unique_id(char out[128]);
 int diag_record_len();
@@ -948,7 +949,17 @@ int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
         c->comm = nullptr;
     }
     QG_CHECK(comm_init(&c->comm, nranks, rank, id));
-    return comm_attach(c, nranks, rank);
+    QG_CHECK(comm_attach(c, nranks, rank));
+    if (const char *e = std::getenv("QG_HALO_PEER"))  // (every rank sees the same environment)
+        if (std::atoi(e) != 0) return qg_comm_set_halo_transport(c, QG_HALO_PEER);
+    return QG_OK;
+}
+
+int qg_comm_set_halo_transport(qg_ctx *c, int transport) {
+    if (!c || (transport != QG_HALO_RCCL && transport != QG_HALO_PEER)) return QG_ERR_INVALID_ARG;
+    if (!c->distributed || !c->comm) return QG_ERR_RCCL;
+    QG_HIP(hipSetDevice(c->device));
+    return comm_set_peer(c->comm, transport == QG_HALO_PEER, c->row_words());
 }
 
 int qg_comm_init_host(qg_ctx *c, int nranks, int rank, qg_allgather_fn allgather, qg_sendrecv_fn sendrecv,

@@ -4,7 +4,8 @@
 //     diagonal corners the Arakawa Jacobian reads arrive with it);
 //   - ghost-row refresh of the fields written by the previous step (drop-in ghost ring),
 //     grouped with the next step's halo exchange;
-//   - the spectral solver's per-step all-gather of the rank records (a few hundred KB).
+//   - the spectral solver's per-step all-gather of the rank records (a few hundred KB);
+//   - optionally (comm_set_peer) the halo rows by copy engine into IPC-mapped peer buffers.
 #include <rccl/rccl.h>
 #include <sched.h>
 
@@ -12,6 +13,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <vector>
 
 #include "qg_common.hpp"
 
@@ -31,7 +33,25 @@ struct Comm {
     int64_t seq = 0;
     double timeout_s = 120.0;
     bool failed = false;
+    // peer-copy halo transport (comm_set_peer): the halo rows go by copy engine straight into
+    // the neighbours' receive regions, opened through IPC; a one-lane kernel then raises the
+    // neighbour's arrival flag, and a one-lane kernel on the receiving side polls its flags
+    // before the halo is read.  No RCCL kernel, so no compute-unit slots are needed beside
+    // the interior tendency.  Receive region (uncached device memory, so the copy engine's
+    // writes are never hidden behind a stale L2 line): [flags: 2 x 64 B | parity 0: from_prev,
+    // from_next | parity 1: ...], each direction PEER_ROWS rows of ld words.
+    bool peer = false;
+    double *prx = nullptr;             // this rank's receive region
+    double *prx_peer[2] = {nullptr, nullptr};  // the receive regions of next (0) and prev (1)
+    bool prx_opened[2] = {false, false};        // IPC-mapped (false: this rank's own region)
+    int64_t peer_ld = 0;
+    int64_t pseq = 0;  // peer exchanges posted (the arrival flags' values)
+    int64_t *perr_h = nullptr, *perr_d = nullptr;  // wait-kernel timeout: the exchange number
+    uint64_t clock_khz = 100000;
 };
+
+constexpr int PEER_ROWS = 8;       // rows per direction (4 fields x 2)
+constexpr int64_t PEER_HDR = 16;   // words before the rows: flag from_prev @0, from_next @8
 
 #define QG_NCCL(call)                                                                          \
     do {                                                                                       \
@@ -139,9 +159,26 @@ int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sen
     return QG_OK;
 }
 
+static void peer_release(Comm *c) {
+    if (c->prx) (void)hipDeviceSynchronize();  // (queued copies may still target the regions)
+    for (int k = 0; k < 2; ++k) {
+        if (c->prx_opened[k] && c->prx_peer[k] && !(k == 1 && c->prx_peer[1] == c->prx_peer[0]))
+            (void)hipIpcCloseMemHandle(c->prx_peer[k]);
+        c->prx_peer[k] = nullptr;
+        c->prx_opened[k] = false;
+    }
+    if (c->prx) (void)hipFree(c->prx);
+    c->prx = nullptr;
+    if (c->perr_h) (void)hipHostFree(c->perr_h);
+    c->perr_h = c->perr_d = nullptr;
+    c->peer = false;
+    c->peer_ld = 0;
+}
+
 int comm_destroy(void *comm) {
     Comm *c = static_cast<Comm *>(comm);
     if (!c) return QG_OK;
+    peer_release(c);
     if (c->nccl) ncclCommDestroy(c->nccl);
     if (c->stage) (void)hipFree(c->stage);
     if (c->progress_h) (void)hipHostFree(c->progress_h);
@@ -221,6 +258,17 @@ int comm_wait(void *comm, hipStream_t s, hipEvent_t ev, const char *what) {
             return QG_ERR_HIP;
         }
         const auto now = clk::now();
+        if (c->perr_h && __atomic_load_n(c->perr_h, __ATOMIC_RELAXED) != 0) {
+            std::fprintf(stderr,
+                         "qg_mi355 rank %d/%d: %s: peer-copy halo #%lld did not arrive within %.1f s -- a peer "
+                         "died or posted a different schedule; aborting the communicator\n",
+                         c->rank, c->nranks, what, (long long)__atomic_load_n(c->perr_h, __ATOMIC_RELAXED),
+                         c->timeout_s);
+            if (c->nccl) ncclCommAbort(c->nccl);
+            c->nccl = nullptr;
+            c->failed = true;
+            return QG_ERR_RCCL;
+        }
         ncclResult_t ar = ncclSuccess;
         if (c->nccl && ncclCommGetAsyncError(c->nccl, &ar) == ncclSuccess && ar != ncclSuccess &&
             ar != ncclInProgress) {
@@ -354,10 +402,14 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
 // tendency reads them from the staging buffer) and no ghost rows (refreshed by the next
 // ghost flush).  rows_out[4 f + h] = row h of field f (h: -2, -1, P, P+1).  The pack kernel
 // publishes the watchdog's progress: every earlier exchange has completed when it runs.
+static int peer_halo_rows(Comm *c, double *const *f2, int n2, int64_t ld, int64_t P, hipStream_t s,
+                          const double **rows_out);
+
 int comm_halo_rows(void *comm, double *const *f2, int n2, int64_t ld, int64_t P, hipStream_t s,
                    const double **rows_out) {
     Comm *c = static_cast<Comm *>(comm);
     if (!c || c->failed || (!c->nccl && !c->sr)) return QG_ERR_RCCL;
+    if (c->peer) return peer_halo_rows(c, f2, n2, ld, P, s, rows_out);
     const int rows = 2 * n2;
     if (n2 < 1 || 2 * rows > XMAX) return QG_ERR_INVALID_ARG;
     double *xbuf[4];
@@ -379,6 +431,187 @@ int comm_halo_rows(void *comm, double *const *f2, int n2, int64_t ld, int64_t P,
     QG_CHECK(copy_rows(pk, s, c->progress_d, c->seq));
     ++c->seq;
     return post(c, xbuf, (int64_t)rows * ld, s);
+}
+
+// ---- peer-copy halo transport ----------------------------------------------------------
+// Raise the arrival flags of exchange `seq` in the neighbours' receive regions.  Stream order
+// puts this launch after the copy-engine copies into those regions have completed.
+__global__ void peer_signal_kernel(uint64_t *flag_next, uint64_t *flag_prev, uint64_t seq) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag_next, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 1) __hip_atomic_store(flag_prev, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Wait (one lane) until both neighbours have raised this rank's flags to >= seq; bounded by
+// `limit` wall-clock ticks, after which the exchange number goes to *err (read by comm_wait,
+// which then fails the transport) and the kernel ends, so a dead peer never leaves a wave
+// spinning.  On arrival the watchdog's progress word advances.
+__global__ void peer_wait_kernel(const uint64_t *flags, uint64_t seq, uint64_t limit, int64_t *progress,
+                                 int64_t prog, int64_t *err) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = wall_clock64();
+    for (;;) {
+        const uint64_t a = __hip_atomic_load(flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t b = __hip_atomic_load(flags + 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (a >= seq && b >= seq) break;
+        if (wall_clock64() - t0 > limit) {
+            __hip_atomic_store(err, (int64_t)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+    if (progress) __hip_atomic_store(progress, prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static double *peer_region(double *base, int64_t ld, int par, int dir) {
+    return base + PEER_HDR + (size_t)(2 * par + dir) * PEER_ROWS * ld;
+}
+
+// all ranks have reached this point (a one-word all-gather, waited on with the watchdog)
+static int comm_barrier(Comm *c) {
+    double *b = nullptr;
+    hipStream_t s = nullptr;
+    QG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    int st = hipMalloc((void **)&b, sizeof(double) * (size_t)(1 + c->nranks)) == hipSuccess ? QG_OK : QG_ERR_ALLOC;
+    if (st == QG_OK && hipMemsetAsync(b, 0, sizeof(double), s) != hipSuccess) st = QG_ERR_HIP;
+    if (st == QG_OK && ncclAllGather(b, b + 1, 1, ncclDouble, c->nccl, s) != ncclSuccess) st = QG_ERR_RCCL;
+    if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_set_halo_transport (barrier)");
+    if (b) (void)hipFree(b);
+    (void)hipStreamDestroy(s);
+    return st;
+}
+
+// Collective (every rank, same arguments): switch the halo rows of comm_halo_rows to the
+// peer-copy transport for rows of `ld` words, or back to RCCL (on = 0).  RCCL transport only:
+// the receive regions' IPC handles are all-gathered over it.  Every rank ends in the same
+// mode: a rank whose set-up failed makes all of them return QG_ERR_UNSUPPORTED.
+int comm_set_peer(void *comm, int on, int64_t ld) {
+    Comm *c = static_cast<Comm *>(comm);
+    if (!c || c->failed) return QG_ERR_RCCL;
+    if (!on && !c->peer) return QG_OK;
+    if (on && !c->nccl) return QG_ERR_UNSUPPORTED;
+    if (on && ld < 1) return QG_ERR_INVALID_ARG;
+    if (on && c->peer && c->peer_ld == ld) return QG_OK;
+    if (c->peer) {  // a neighbour's copies may still be landing in this rank's region: every
+        // rank drains its device, then one all-gather, before any region is released
+        QG_HIP(hipDeviceSynchronize());
+        const int b = comm_barrier(c);
+        peer_release(c);
+        if (b != QG_OK) return b;
+    }
+    if (!on) return QG_OK;
+    const int G = c->nranks;
+    hipStream_t s = nullptr;
+    QG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    double *hb = nullptr;  // [own handle | all handles | own status | all statuses], 8 words each
+    int st = QG_OK;
+    const size_t bytes = sizeof(double) * (size_t)(PEER_HDR + 4 * PEER_ROWS * ld);
+    std::vector<hipIpcMemHandle_t> all((size_t)G);
+    static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+    if (hipMalloc((void **)&hb, sizeof(double) * 8 * (size_t)(2 * G + 2)) != hipSuccess) st = QG_ERR_ALLOC;
+    int local = QG_OK;
+    if (st == QG_OK) {
+        int dev = 0, khz = 0;
+        if (hipExtMallocWithFlags((void **)&c->prx, bytes, hipDeviceMallocUncached) != hipSuccess) c->prx = nullptr;
+        if (!c->prx || hipMemset(c->prx, 0, bytes) != hipSuccess) local = QG_ERR_ALLOC;
+        if (local == QG_OK && (hipHostMalloc((void **)&c->perr_h, sizeof(int64_t),
+                                             hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+                               hipHostGetDevicePointer((void **)&c->perr_d, c->perr_h, 0) != hipSuccess))
+            local = QG_ERR_ALLOC;
+        if (local == QG_OK) *c->perr_h = 0;
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+            c->clock_khz = (uint64_t)khz;
+        hipIpcMemHandle_t h{};
+        if (local == QG_OK && hipIpcGetMemHandle(&h, c->prx) != hipSuccess) local = QG_ERR_UNSUPPORTED;
+        if (hipMemcpy(hb, &h, 64, hipMemcpyHostToDevice) != hipSuccess) st = QG_ERR_HIP;
+    }
+    if (st == QG_OK && ncclAllGather(hb, hb + 8, 8, ncclDouble, c->nccl, s) != ncclSuccess) st = QG_ERR_RCCL;
+    if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_set_halo_transport (handles)");
+    if (st == QG_OK && hipMemcpy(all.data(), hb + 8, 64 * (size_t)G, hipMemcpyDeviceToHost) != hipSuccess)
+        st = QG_ERR_HIP;
+    const int next = (c->rank + 1) % G, prev = (c->rank - 1 + G) % G;
+    if (st == QG_OK && local == QG_OK) {
+        for (int k = 0; k < 2 && local == QG_OK; ++k) {
+            const int pr = k == 0 ? next : prev;
+            if (pr == c->rank) {
+                c->prx_peer[k] = c->prx;
+            } else if (k == 1 && prev == next) {
+                c->prx_peer[1] = c->prx_peer[0];
+                c->prx_opened[1] = true;
+            } else if (hipIpcOpenMemHandle((void **)&c->prx_peer[k], all[(size_t)pr],
+                                           hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
+                c->prx_opened[k] = true;
+            } else {
+                c->prx_peer[k] = nullptr;
+                local = QG_ERR_UNSUPPORTED;
+            }
+        }
+    }
+    if (st == QG_OK) {  // agree: the transport switches only if every rank's set-up succeeded
+        double v[8] = {(double)local};
+        if (hipMemcpy(hb + 8 * (size_t)(G + 1), v, 64, hipMemcpyHostToDevice) != hipSuccess) st = QG_ERR_HIP;
+        if (st == QG_OK &&
+            ncclAllGather(hb + 8 * (size_t)(G + 1), hb + 8 * (size_t)(G + 2), 8, ncclDouble, c->nccl, s) != ncclSuccess)
+            st = QG_ERR_RCCL;
+        if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_set_halo_transport (status)");
+        std::vector<double> sts(8 * (size_t)G);
+        if (st == QG_OK &&
+            hipMemcpy(sts.data(), hb + 8 * (size_t)(G + 2), sizeof(double) * sts.size(), hipMemcpyDeviceToHost) !=
+                hipSuccess)
+            st = QG_ERR_HIP;
+        for (int r = 0; st == QG_OK && r < G; ++r)
+            if (sts[8 * (size_t)r] != 0.0) {
+                if (r == c->rank || local == QG_OK)
+                    std::fprintf(stderr, "qg_mi355 rank %d/%d: peer-copy halo transport unavailable (rank %d: %s)\n",
+                                 c->rank, G, r, qg_strerror((int)sts[8 * (size_t)r]));
+                st = QG_ERR_UNSUPPORTED;
+                break;
+            }
+    }
+    if (hb) (void)hipFree(hb);
+    (void)hipStreamDestroy(s);
+    if (st != QG_OK) {
+        peer_release(c);
+        return st;
+    }
+    c->peer = true;
+    c->peer_ld = ld;
+    c->pseq = 0;
+    return QG_OK;
+}
+
+// One halo exchange over the peer-copy transport: per field, this rank's top two rows go to
+// next's from_prev rows and its bottom two rows to prev's from_next rows (copy engine, no
+// compute units), then the flags; the rows of exchange seq land in parity seq & 1, so the
+// next exchange never writes rows a neighbour may still be reading (every step also runs a
+// collective between two exchanges).  rows_out as comm_halo_rows.
+static int peer_halo_rows(Comm *c, double *const *f2, int n2, int64_t ld, int64_t P, hipStream_t s,
+                          const double **rows_out) {
+    if (n2 < 1 || 2 * n2 > PEER_ROWS) return QG_ERR_INVALID_ARG;
+    if (ld != c->peer_ld) return QG_ERR_INVALID_ARG;
+    const int64_t seq = ++c->pseq;
+    const int par = (int)(seq & 1);
+    double *to_next = peer_region(c->prx_peer[0], ld, par, 0), *to_prev = peer_region(c->prx_peer[1], ld, par, 1);
+    const double *from_prev = peer_region(c->prx, ld, par, 0), *from_next = peer_region(c->prx, ld, par, 1);
+    const size_t bytes = sizeof(double) * 2 * (size_t)ld;
+    for (int f = 0; f < n2; ++f) {
+        const double *b = f2[f];
+        QG_HIP(hipMemcpyAsync(to_next + 2 * f * ld, b + fidx(0, P - 1, ld), bytes, hipMemcpyDeviceToDeviceNoCU, s));
+        QG_HIP(hipMemcpyAsync(to_prev + 2 * f * ld, b + fidx(0, 1, ld), bytes, hipMemcpyDeviceToDeviceNoCU, s));
+        for (int q = 0; q < 2; ++q) {
+            rows_out[4 * f + q] = from_prev + (2 * f + q) * ld;      // rows -2, -1
+            rows_out[4 * f + 2 + q] = from_next + (2 * f + q) * ld;  // rows P, P+1
+        }
+    }
+    peer_signal_kernel<<<1, 64, 0, s>>>(reinterpret_cast<uint64_t *>(c->prx_peer[0]),
+                                        reinterpret_cast<uint64_t *>(c->prx_peer[1]) + 8, (uint64_t)seq);
+    QG_LAUNCH_CHECK();
+    const uint64_t limit = (uint64_t)(c->timeout_s * (double)c->clock_khz * 1000.0);
+    peer_wait_kernel<<<1, 64, 0, s>>>(reinterpret_cast<const uint64_t *>(c->prx), (uint64_t)seq, limit,
+                                      c->progress_d, c->seq + 1, c->perr_d);
+    QG_LAUNCH_CHECK();
+    ++c->seq;
+    return QG_OK;
 }
 
 // depth == 2: halo rows into halo_buf; depth == -1: ghost-row refresh in place

@@ -237,6 +237,12 @@ tendency runs (bit-identical; include/qg_mi355.h qg_set_overlap)."""
 set_overlap!(s::QGState, on::Bool=true) =
     @qgcheck qg_set_overlap ccall((:qg_set_overlap, libqg), Cint, (Ptr{Cvoid}, Cint), s.ctx, Cint(on))
 
+"""`set_halo_transport!(s, peer)`: collective; `peer = true` sends the halo rows by copy engine into
+the neighbours' IPC-mapped receive regions (include/qg_mi355.h qg_comm_set_halo_transport)."""
+set_halo_transport!(s::QGState, peer::Bool) =
+    @qgcheck qg_comm_set_halo_transport ccall((:qg_comm_set_halo_transport, libqg), Cint, (Ptr{Cvoid}, Cint),
+                                              s.ctx, Cint(peer ? 1 : 0))
+
 """`run_model_no_output(model)` (run_model_no_output.jl:3-16) -> (zeta, psi) on the device,
 slots in the reference's order."""
 function run_model_no_output(model; kw...)

@@ -252,6 +252,16 @@ class State:
         interior rows' tendency meanwhile (multi-rank only; bit-identical results)."""
         call("qg_set_overlap", self._ctx, 1 if on else 0)
 
+    def set_halo_transport(self, transport="rccl"):
+        """qg_comm_set_halo_transport (collective, RCCL transport only): "rccl" (pack kernel +
+        grouped send/recv) or "peer" (copy-engine copies into the neighbours' IPC-mapped
+        receive regions + arrival flags; no collective kernel beside the interior tendency)."""
+        modes = {"rccl": 0, "peer": 1}
+        if transport not in modes:
+            raise ValueError(f"halo transport {transport!r}: one of {sorted(modes)}")
+        call("qg_comm_set_halo_transport", self._ctx, modes[transport])
+        self.halo_transport = transport
+
     def comm_probe(self, reps=20):
         """qg_comm_probe: event-timed halo exchange and record all-gather of one step, in
         isolation (every rank must call it): ms and bytes per collective."""

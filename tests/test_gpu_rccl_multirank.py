@@ -27,7 +27,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, M, P, steps, outdir, solver, overlap):
+def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl"):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
@@ -54,6 +54,8 @@ def _worker(rank, world, port, M, P, steps, outdir, solver, overlap):
     m = qgamd.bench_model(M, P=P)
     st = qgamd.State(m, P_local=P // world, solver=solver)
     st.comm_init(world, rank, bytes(uid.numpy().tobytes()))
+    if halo != "rccl":
+        st.set_halo_transport(halo)
     st.set_overlap(overlap)
     st.initialise()
     st.run(1, steps)
@@ -64,12 +66,13 @@ def _worker(rank, world, port, M, P, steps, outdir, solver, overlap):
     dist.destroy_process_group()
 
 
-def _run(world, M, P, steps, d, solver, overlap):
+def _run(world, M, P, steps, d, solver, overlap, halo="rccl"):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap, halo))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -118,6 +121,24 @@ def test_rccl_overlap_is_bit_identical():
         a = _run(2, 64, 64, 6, d0, 0, False)
         b = _run(2, 64, 64, 6, d1, 0, True)
     for r in range(2):
+        for n in ("zeta", "psi", "f_store"):
+            assert np.array_equal(a[r][n], b[r][n]), (r, n)
+
+
+@pytest.mark.parametrize("world,overlap", [(2, True), (4, True), (4, False)])
+def test_peer_halo_across_processes_bit_identical(world, overlap):
+    """The peer-copy halo transport between rank processes: each rank's receive region is
+    opened by its neighbours through IPC (here all on the one GPU), the rows arrive by copy
+    engine with an arrival flag; every slot of every slab bit for bit equal to the RCCL
+    send/recv transport (2 ranks: both neighbours are the same peer)."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    with tempfile.TemporaryDirectory() as d0, tempfile.TemporaryDirectory() as d1:
+        a = _run(world, 64, 64, 6, d0, 0, overlap, "rccl")
+        b = _run(world, 64, 64, 6, d1, 0, overlap, "peer")
+    for r in range(world):
         for n in ("zeta", "psi", "f_store"):
             assert np.array_equal(a[r][n], b[r][n]), (r, n)
 
@@ -240,7 +261,7 @@ def _rccl_state(rank, world, port, m, **kw):
     return torch, dist, qgamd, st
 
 
-def _silent_peer_worker(rank, world, port, outdir):
+def _silent_peer_worker(rank, world, port, outdir, halo="rccl"):
     """rank 1 joins the communicator and then never steps; rank 0 must get QG_ERR_RCCL from its
     watchdog (ncclCommAbort), not hang in the halo exchange."""
     import ctypes as C
@@ -248,6 +269,9 @@ def _silent_peer_worker(rank, world, port, outdir):
     import time
 
     torch, dist, qgamd, st = _rccl_state(rank, world, port, lambda q: q.bench_model(64, P=64), P_local=32)
+    if halo != "rccl":
+        qgamd._lib.call("qg_comm_set_timeout", st._ctx, C.c_double(2.0))  # (the wait kernel's bound too)
+        st.set_halo_transport(halo)
     st.initialise()
     dist.barrier()
     if rank == 1:
@@ -266,7 +290,8 @@ def _silent_peer_worker(rank, world, port, outdir):
     os._exit(0)
 
 
-def test_rccl_silent_peer_returns_rccl_error():
+@pytest.mark.parametrize("halo", ["rccl", "peer"])
+def test_rccl_silent_peer_returns_rccl_error(halo):
     import json
 
     import torch
@@ -279,7 +304,7 @@ def test_rccl_silent_peer_returns_rccl_error():
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
         port = _free_port()
-        procs = [ctx.Process(target=_silent_peer_worker, args=(r, 2, port, d)) for r in range(2)]
+        procs = [ctx.Process(target=_silent_peer_worker, args=(r, 2, port, d, halo)) for r in range(2)]
         for p in procs:
             p.start()
         for p in procs:

@@ -43,3 +43,65 @@ def test_one_rank_rccl_ring_matches_single_gpu(overlap):
         st2.run(1, 7)
         for n in ("zeta", "psi", "f_store"):
             assert np.array_equal(st.to_numpy(n), st2.to_numpy(n)), n
+
+
+def _ring_state(qgamd, m, transport, overlap, **kw):
+    st = qgamd.State(m, **kw)
+    uid = C.create_string_buffer(128)
+    qgamd._lib.call("qg_comm_unique_id", uid)
+    st.comm_init(1, 0, uid.raw)
+    st.set_halo_transport(transport)
+    st.set_overlap(overlap)
+    st.initialise()
+    return st
+
+
+@pytest.mark.parametrize("M,P,f32,overlap", [(64, 48, False, True), (64, 48, False, False), (96, 64, True, True),
+                                             (1024, 256, False, True)])
+def test_one_rank_peer_halo_bit_identical(M, P, f32, overlap):
+    """The peer-copy halo transport (copy engine into the IPC-style receive region, arrival
+    flags, one-lane wait kernel) over the one-rank ring: every slot bit for bit equal to the
+    RCCL send/recv transport, for both schedules and both precisions."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+
+    m = qgamd.bench_model(M, P=P)
+    kw = {"dtype": torch.float32} if f32 else {}
+    a = _ring_state(qgamd, m, "rccl", overlap, **kw)
+    a.run(1, 9)
+    b = _ring_state(qgamd, m, "peer", overlap, **kw)
+    b.run(1, 9)
+    torch.cuda.synchronize()
+    for n in ("zeta", "psi", "f_store"):
+        assert np.array_equal(a.to_numpy(n), b.to_numpy(n)), n
+
+
+def test_one_rank_peer_halo_switch_and_probe():
+    """Switching the transport between steps (collective re-setup and release), the comm probe's
+    back-to-back exchanges in peer mode, and a second switch back: the trajectory stays bit for
+    bit the RCCL one."""
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+
+    m = qgamd.bench_model(128, P=64)
+    a = _ring_state(qgamd, m, "rccl", True)
+    a.run(1, 12)
+    b = _ring_state(qgamd, m, "rccl", True)
+    b.run(1, 4)
+    b.set_halo_transport("peer")
+    pr = b.comm_probe(5)
+    assert pr["halo_ms"] > 0
+    b.run(5, 4)
+    b.set_halo_transport("rccl")
+    b.run(9, 2)
+    b.set_halo_transport("peer")
+    b.run(11, 2)
+    torch.cuda.synchronize()
+    for n in ("zeta", "psi", "f_store"):
+        assert np.array_equal(a.to_numpy(n), b.to_numpy(n)), n

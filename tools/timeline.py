@@ -1,11 +1,18 @@
 """Print a per-step kernel timeline from a rocprofv3 kernel_trace.csv.
-usage: python tools/timeline.py TRACE.csv [first_kernel_substring] [nsteps]"""
+usage: python tools/timeline.py TRACE.csv [first_kernel_substring] [nsteps] [MEMORY_COPY_TRACE.csv]
+(the memory-copy trace's copies are merged in as "COPY <direction>" rows)"""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 key = sys.argv[2] if len(sys.argv) > 2 else "tendency_kernel"
 nsteps = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+if len(sys.argv) > 4:
+    for r in csv.DictReader(open(sys.argv[4])):
+        r = dict(r)
+        r["Kernel_Name"] = f"COPY {r.get('Direction', '?')} {r.get('Bytes', r.get('Size', ''))}"
+        r.setdefault("Queue_Id", "cp")
+        rows.append(r)
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 starts = [k for k, r in enumerate(rows) if key in r["Kernel_Name"]]
 # the last nsteps+1 occurrences delimit nsteps steps
