@@ -93,6 +93,10 @@ def parse():
                     help="RCCL transport: how the halo rows travel (qg_comm_set_halo_transport): rccl = "
                          "pack + grouped send/recv; peer = copy-engine copies into the neighbours' "
                          "IPC-mapped receive regions + arrival flags")
+    ap.add_argument("--gather", choices=["rccl", "peer"], default="rccl",
+                    help="RCCL transport, direct solver: how the per-step record all-gather travels "
+                         "(qg_comm_set_gather_transport): rccl = ncclAllGather; peer = one kernel storing "
+                         "into every peer's IPC-mapped region")
     ap.add_argument("--dropin-steps", type=int, default=20,
                     help="also time this many steps through the reference's own array signatures "
                          "(evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(...) on bare arrays, "
@@ -373,6 +377,9 @@ def main():
         st.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
     if args.halo != "rccl" and args.transport == "rccl" and (world > 1 or args.comm_self):
         st.set_halo_transport(args.halo)
+    if args.gather != "rccl" and args.transport == "rccl" and (world > 1 or args.comm_self) \
+            and args.solver == "spectral":
+        st.set_gather_transport(args.gather)
     st.set_overlap(args.overlap)
     st.initialise()
     torch.cuda.synchronize()
@@ -575,6 +582,8 @@ def main():
             "halo_overlap": bool(args.overlap and (world > 1 or args.comm_self)),
             "halo_transport": (getattr(st, "halo_transport", "rccl") if args.transport == "rccl"
                                and (world > 1 or args.comm_self) else None),
+            "gather_transport": (getattr(st, "gather_transport", "rccl") if args.transport == "rccl"
+                                 and (world > 1 or args.comm_self) and args.solver == "spectral" else None),
         },
         "roofline": {
             "bound": "hbm",

@@ -270,6 +270,16 @@ int qg_set_overlap(qg_ctx *ctx, int on);
  * open the regions.  The environment variable QG_HALO_PEER=1 selects it in qg_comm_init. */
 enum { QG_HALO_RCCL = 0, QG_HALO_PEER = 1 };
 int qg_comm_set_halo_transport(qg_ctx *ctx, int transport);
+/* How the direct solver's per-step record all-gather travels (collective, RCCL transport
+ * only, spectral solver only: QG_ERR_UNSUPPORTED for PCG).
+ * QG_GATHER_RCCL (default): ncclAllGather.
+ * QG_GATHER_PEER: one kernel per solve; its workgroups store this rank's record straight into
+ * every peer's IPC-mapped receive region (all peers in parallel, each over its own link,
+ * instead of a ring of nranks - 1 steps), raise the peer's flag, then wait for the peers'
+ * flags and copy their records out (waits bounded by the comm timeout).  The environment
+ * variable QG_GATHER_PEER=1 selects it in qg_comm_init. */
+enum { QG_GATHER_RCCL = 0, QG_GATHER_PEER = 1 };
+int qg_comm_set_gather_transport(qg_ctx *ctx, int transport);
 /* Time the two collectives of a multi-GPU step in isolation (HIP events on the context's
  * stream, `reps` back-to-back calls each; every rank calls it): out[0] = ms per halo exchange
  * (pack + grouped send/recv of the depth-2 rows of psi and zeta), out[1] = bytes this rank

@@ -24,6 +24,8 @@ int comm_exchange(void *comm, double *const *f2, int n2, double *halo_buf, doubl
                   int64_t P, hipStream_t s, bool ghost_f2);
 int comm_init(void **comm, int nranks, int rank, const char id[128]);
 int comm_set_peer(void *comm, int on, int64_t ld);
+int comm_set_peer_gather(void *comm, int on, int64_t count);
+int comm_gather_records(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
 int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sendrecv_fn sr, void *user);
 int comm_unique_id(char out[128]);
 int diag_record_len();
@@ -581,7 +583,7 @@ int qg_evolve_psi(qg_ctx *c) {
         if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
     } else {
         QG_CHECK(c->spec->solve(z1, z2, o1, o2, !c->distributed, c->stream,
-                                c->distributed ? comm_allgather : nullptr, c->comm));
+                                c->distributed ? comm_gather_records : nullptr, c->comm));
     }
     c->heads[1] = pn;
     if (c->distributed) c->ghosts_pending = true;  // psi's ghost rows: at the next ghost flush
@@ -951,8 +953,18 @@ int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
     QG_CHECK(comm_init(&c->comm, nranks, rank, id));
     QG_CHECK(comm_attach(c, nranks, rank));
     if (const char *e = std::getenv("QG_HALO_PEER"))  // (every rank sees the same environment)
-        if (std::atoi(e) != 0) return qg_comm_set_halo_transport(c, QG_HALO_PEER);
+        if (std::atoi(e) != 0) QG_CHECK(qg_comm_set_halo_transport(c, QG_HALO_PEER));
+    if (const char *e = std::getenv("QG_GATHER_PEER"))
+        if (std::atoi(e) != 0 && c->spec) QG_CHECK(qg_comm_set_gather_transport(c, QG_GATHER_PEER));
     return QG_OK;
+}
+
+int qg_comm_set_gather_transport(qg_ctx *c, int transport) {
+    if (!c || (transport != QG_GATHER_RCCL && transport != QG_GATHER_PEER)) return QG_ERR_INVALID_ARG;
+    if (!c->distributed || !c->comm) return QG_ERR_RCCL;
+    if (!c->spec) return QG_ERR_UNSUPPORTED;
+    QG_HIP(hipSetDevice(c->device));
+    return comm_set_peer_gather(c->comm, transport == QG_GATHER_PEER, c->spec->args().rec_stride);
 }
 
 int qg_comm_set_halo_transport(qg_ctx *c, int transport) {
@@ -999,12 +1011,12 @@ int qg_comm_probe(qg_ctx *c, int reps, double out[4]) {
     int st = QG_OK;
     auto run = [&]() -> int {
         QG_CHECK(comm_halo_rows(c->comm, f2, 4, c->row_words(), p.P, c->stream, hr));  // (warm)
-        QG_CHECK(comm_allgather(c->comm, sa.rec, c->spec->gather_buf(), sa.rec_stride, c->stream));
+        QG_CHECK(comm_gather_records(c->comm, sa.rec, c->spec->gather_buf(), sa.rec_stride, c->stream));
         QG_HIP(hipEventRecord(ev[0], c->stream));
         for (int k = 0; k < reps; ++k) QG_CHECK(comm_halo_rows(c->comm, f2, 4, c->row_words(), p.P, c->stream, hr));
         QG_HIP(hipEventRecord(ev[1], c->stream));
         for (int k = 0; k < reps; ++k)
-            QG_CHECK(comm_allgather(c->comm, sa.rec, c->spec->gather_buf(), sa.rec_stride, c->stream));
+            QG_CHECK(comm_gather_records(c->comm, sa.rec, c->spec->gather_buf(), sa.rec_stride, c->stream));
         QG_HIP(hipEventRecord(ev[2], c->stream));
         QG_CHECK(comm_wait(c->comm, c->stream, ev[2], "qg_comm_probe"));
         float a = 0, b = 0;

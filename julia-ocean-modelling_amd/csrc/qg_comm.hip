@@ -5,7 +5,8 @@
 //   - ghost-row refresh of the fields written by the previous step (drop-in ghost ring),
 //     grouped with the next step's halo exchange;
 //   - the spectral solver's per-step all-gather of the rank records (a few hundred KB);
-//   - optionally (comm_set_peer) the halo rows by copy engine into IPC-mapped peer buffers.
+//   - optionally (comm_set_peer / comm_set_peer_gather) the halo rows by copy engine and the
+//     records by one kernel, both into IPC-mapped peer buffers.
 #include <rccl/rccl.h>
 #include <sched.h>
 
@@ -33,25 +34,39 @@ struct Comm {
     int64_t seq = 0;
     double timeout_s = 120.0;
     bool failed = false;
-    // peer-copy halo transport (comm_set_peer): the halo rows go by copy engine straight into
-    // the neighbours' receive regions, opened through IPC; a one-lane kernel then raises the
-    // neighbour's arrival flag, and a one-lane kernel on the receiving side polls its flags
-    // before the halo is read.  No RCCL kernel, so no compute-unit slots are needed beside
-    // the interior tendency.  Receive region (uncached device memory, so the copy engine's
-    // writes are never hidden behind a stale L2 line): [flags: 2 x 64 B | parity 0: from_prev,
-    // from_next | parity 1: ...], each direction PEER_ROWS rows of ld words.
+    // Peer transports (RCCL communicator only).  Each uses an IpcRegion: uncached device memory
+    // of this rank (so writes from other agents are never hidden behind a stale L2 line),
+    // opened by the ranks that write into it through IPC.
+    // - halo (comm_set_peer): the halo rows go by copy engine straight from the state into
+    //   the ring neighbours' regions; a one-lane kernel then raises the neighbour's arrival
+    //   flag and a one-lane kernel on the receiving side polls its flags before the halo is
+    //   read.  No collective kernel, so no compute-unit slots are needed beside the interior
+    //   tendency.  Region: [flags: 2 x 64 B | parity 0: from_prev, from_next | parity 1: ...],
+    //   each direction PEER_ROWS rows of ld words.
+    // - record gather (comm_set_peer_gather): one kernel per solve, (blocks x ranks)
+    //   workgroups; workgroup (b, r) stores part b of this rank's record into rank r's region,
+    //   raises r's flag (rank, b), waits for r's flag in this rank's region and copies r's
+    //   part b out.  One launch, every peer written in parallel over its own link (no ring).
+    struct IpcRegion {
+        double *local = nullptr;
+        std::vector<double *> remote;  // per rank: its region as mapped here (self: local)
+        std::vector<char> opened;      // remote[r] is an IPC mapping to close
+    };
+    IpcRegion halo_rx, gat_rx;
     bool peer = false;
-    double *prx = nullptr;             // this rank's receive region
-    double *prx_peer[2] = {nullptr, nullptr};  // the receive regions of next (0) and prev (1)
-    bool prx_opened[2] = {false, false};        // IPC-mapped (false: this rank's own region)
     int64_t peer_ld = 0;
-    int64_t pseq = 0;  // peer exchanges posted (the arrival flags' values)
-    int64_t *perr_h = nullptr, *perr_d = nullptr;  // wait-kernel timeout: the exchange number
+    int64_t pseq = 0;  // peer halo exchanges posted (the arrival flags' values)
+    bool pgather = false;
+    int64_t pg_count = 0;
+    int64_t gseq = 0;  // peer record gathers posted
+    int64_t *perr_h = nullptr, *perr_d = nullptr;  // a wait timed out: the exchange number
     uint64_t clock_khz = 100000;
 };
 
 constexpr int PEER_ROWS = 8;       // rows per direction (4 fields x 2)
 constexpr int64_t PEER_HDR = 16;   // words before the rows: flag from_prev @0, from_next @8
+constexpr int PG_BLOCKS = 4;       // record gather: workgroups per peer
+constexpr int PG_MAX_RANKS = 64;
 
 #define QG_NCCL(call)                                                                          \
     do {                                                                                       \
@@ -159,26 +174,29 @@ int comm_init_host(void **comm, int nranks, int rank, qg_allgather_fn ag, qg_sen
     return QG_OK;
 }
 
-static void peer_release(Comm *c) {
-    if (c->prx) (void)hipDeviceSynchronize();  // (queued copies may still target the regions)
-    for (int k = 0; k < 2; ++k) {
-        if (c->prx_opened[k] && c->prx_peer[k] && !(k == 1 && c->prx_peer[1] == c->prx_peer[0]))
-            (void)hipIpcCloseMemHandle(c->prx_peer[k]);
-        c->prx_peer[k] = nullptr;
-        c->prx_opened[k] = false;
-    }
-    if (c->prx) (void)hipFree(c->prx);
-    c->prx = nullptr;
+static void region_release(Comm::IpcRegion &g) {
+    for (size_t r = 0; r < g.remote.size(); ++r)
+        if (g.opened[r] && g.remote[r]) (void)hipIpcCloseMemHandle(g.remote[r]);
+    g.remote.clear();
+    g.opened.clear();
+    if (g.local) (void)hipFree(g.local);
+    g.local = nullptr;
+}
+
+static void peer_release_all(Comm *c) {
+    if (c->halo_rx.local || c->gat_rx.local) (void)hipDeviceSynchronize();  // (queued writes)
+    region_release(c->halo_rx);
+    region_release(c->gat_rx);
+    c->peer = c->pgather = false;
+    c->peer_ld = c->pg_count = 0;
     if (c->perr_h) (void)hipHostFree(c->perr_h);
     c->perr_h = c->perr_d = nullptr;
-    c->peer = false;
-    c->peer_ld = 0;
 }
 
 int comm_destroy(void *comm) {
     Comm *c = static_cast<Comm *>(comm);
     if (!c) return QG_OK;
-    peer_release(c);
+    peer_release_all(c);
     if (c->nccl) ncclCommDestroy(c->nccl);
     if (c->stage) (void)hipFree(c->stage);
     if (c->progress_h) (void)hipHostFree(c->progress_h);
@@ -260,7 +278,7 @@ int comm_wait(void *comm, hipStream_t s, hipEvent_t ev, const char *what) {
         const auto now = clk::now();
         if (c->perr_h && __atomic_load_n(c->perr_h, __ATOMIC_RELAXED) != 0) {
             std::fprintf(stderr,
-                         "qg_mi355 rank %d/%d: %s: peer-copy halo #%lld did not arrive within %.1f s -- a peer "
+                         "qg_mi355 rank %d/%d: %s: peer transfer #%lld did not arrive within %.1f s -- a peer "
                          "died or posted a different schedule; aborting the communicator\n",
                          c->rank, c->nranks, what, (long long)__atomic_load_n(c->perr_h, __ATOMIC_RELAXED),
                          c->timeout_s);
@@ -467,82 +485,67 @@ static double *peer_region(double *base, int64_t ld, int par, int dir) {
 }
 
 // all ranks have reached this point (a one-word all-gather, waited on with the watchdog)
-static int comm_barrier(Comm *c) {
+static int comm_barrier(Comm *c, const char *what) {
     double *b = nullptr;
     hipStream_t s = nullptr;
     QG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     int st = hipMalloc((void **)&b, sizeof(double) * (size_t)(1 + c->nranks)) == hipSuccess ? QG_OK : QG_ERR_ALLOC;
     if (st == QG_OK && hipMemsetAsync(b, 0, sizeof(double), s) != hipSuccess) st = QG_ERR_HIP;
     if (st == QG_OK && ncclAllGather(b, b + 1, 1, ncclDouble, c->nccl, s) != ncclSuccess) st = QG_ERR_RCCL;
-    if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_set_halo_transport (barrier)");
+    if (st == QG_OK) st = comm_wait(c, s, nullptr, what);
     if (b) (void)hipFree(b);
     (void)hipStreamDestroy(s);
     return st;
 }
 
-// Collective (every rank, same arguments): switch the halo rows of comm_halo_rows to the
-// peer-copy transport for rows of `ld` words, or back to RCCL (on = 0).  RCCL transport only:
-// the receive regions' IPC handles are all-gathered over it.  Every rank ends in the same
-// mode: a rank whose set-up failed makes all of them return QG_ERR_UNSUPPORTED.
-int comm_set_peer(void *comm, int on, int64_t ld) {
-    Comm *c = static_cast<Comm *>(comm);
-    if (!c || c->failed) return QG_ERR_RCCL;
-    if (!on && !c->peer) return QG_OK;
-    if (on && !c->nccl) return QG_ERR_UNSUPPORTED;
-    if (on && ld < 1) return QG_ERR_INVALID_ARG;
-    if (on && c->peer && c->peer_ld == ld) return QG_OK;
-    if (c->peer) {  // a neighbour's copies may still be landing in this rank's region: every
-        // rank drains its device, then one all-gather, before any region is released
-        QG_HIP(hipDeviceSynchronize());
-        const int b = comm_barrier(c);
-        peer_release(c);
-        if (b != QG_OK) return b;
-    }
-    if (!on) return QG_OK;
+// Collective: allocate this rank's region (`bytes`, uncached, zeroed), all-gather the IPC
+// handles over RCCL and open the regions of the ranks flagged in `need`.  Every rank ends
+// with the same verdict: a rank whose set-up failed makes all of them return
+// QG_ERR_UNSUPPORTED (regions released).
+static int region_create(Comm *c, Comm::IpcRegion &g, size_t bytes, const std::vector<char> &need, const char *what) {
     const int G = c->nranks;
     hipStream_t s = nullptr;
     QG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     double *hb = nullptr;  // [own handle | all handles | own status | all statuses], 8 words each
-    int st = QG_OK;
-    const size_t bytes = sizeof(double) * (size_t)(PEER_HDR + 4 * PEER_ROWS * ld);
+    int st = QG_OK, local = QG_OK;
     std::vector<hipIpcMemHandle_t> all((size_t)G);
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
+    g.remote.assign((size_t)G, nullptr);
+    g.opened.assign((size_t)G, 0);
     if (hipMalloc((void **)&hb, sizeof(double) * 8 * (size_t)(2 * G + 2)) != hipSuccess) st = QG_ERR_ALLOC;
-    int local = QG_OK;
     if (st == QG_OK) {
-        int dev = 0, khz = 0;
-        if (hipExtMallocWithFlags((void **)&c->prx, bytes, hipDeviceMallocUncached) != hipSuccess) c->prx = nullptr;
-        if (!c->prx || hipMemset(c->prx, 0, bytes) != hipSuccess) local = QG_ERR_ALLOC;
-        if (local == QG_OK && (hipHostMalloc((void **)&c->perr_h, sizeof(int64_t),
-                                             hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-                               hipHostGetDevicePointer((void **)&c->perr_d, c->perr_h, 0) != hipSuccess))
+        if (hipExtMallocWithFlags((void **)&g.local, bytes, hipDeviceMallocUncached) != hipSuccess) g.local = nullptr;
+        if (!g.local || hipMemset(g.local, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
             local = QG_ERR_ALLOC;
-        if (local == QG_OK) *c->perr_h = 0;
+        if (local == QG_OK && !c->perr_h) {
+            if (hipHostMalloc((void **)&c->perr_h, sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+                    hipSuccess ||
+                hipHostGetDevicePointer((void **)&c->perr_d, c->perr_h, 0) != hipSuccess)
+                local = QG_ERR_ALLOC;
+            else
+                *c->perr_h = 0;
+        }
+        int dev = 0, khz = 0;
         if (hipGetDevice(&dev) == hipSuccess &&
             hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
             c->clock_khz = (uint64_t)khz;
         hipIpcMemHandle_t h{};
-        if (local == QG_OK && hipIpcGetMemHandle(&h, c->prx) != hipSuccess) local = QG_ERR_UNSUPPORTED;
+        if (local == QG_OK && hipIpcGetMemHandle(&h, g.local) != hipSuccess) local = QG_ERR_UNSUPPORTED;
         if (hipMemcpy(hb, &h, 64, hipMemcpyHostToDevice) != hipSuccess) st = QG_ERR_HIP;
     }
     if (st == QG_OK && ncclAllGather(hb, hb + 8, 8, ncclDouble, c->nccl, s) != ncclSuccess) st = QG_ERR_RCCL;
-    if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_set_halo_transport (handles)");
+    if (st == QG_OK) st = comm_wait(c, s, nullptr, what);
     if (st == QG_OK && hipMemcpy(all.data(), hb + 8, 64 * (size_t)G, hipMemcpyDeviceToHost) != hipSuccess)
         st = QG_ERR_HIP;
-    const int next = (c->rank + 1) % G, prev = (c->rank - 1 + G) % G;
-    if (st == QG_OK && local == QG_OK) {
-        for (int k = 0; k < 2 && local == QG_OK; ++k) {
-            const int pr = k == 0 ? next : prev;
-            if (pr == c->rank) {
-                c->prx_peer[k] = c->prx;
-            } else if (k == 1 && prev == next) {
-                c->prx_peer[1] = c->prx_peer[0];
-                c->prx_opened[1] = true;
-            } else if (hipIpcOpenMemHandle((void **)&c->prx_peer[k], all[(size_t)pr],
-                                           hipIpcMemLazyEnablePeerAccess) == hipSuccess) {
-                c->prx_opened[k] = true;
-            } else {
-                c->prx_peer[k] = nullptr;
+    for (int r = 0; st == QG_OK && local == QG_OK && r < G; ++r) {
+        if (r == c->rank) {
+            g.remote[(size_t)r] = g.local;
+        } else if (need[(size_t)r]) {
+            if (hipIpcOpenMemHandle((void **)&g.remote[(size_t)r], all[(size_t)r], hipIpcMemLazyEnablePeerAccess) ==
+                hipSuccess)
+                g.opened[(size_t)r] = 1;
+            else {
+                g.remote[(size_t)r] = nullptr;
                 local = QG_ERR_UNSUPPORTED;
             }
         }
@@ -553,7 +556,7 @@ int comm_set_peer(void *comm, int on, int64_t ld) {
         if (st == QG_OK &&
             ncclAllGather(hb + 8 * (size_t)(G + 1), hb + 8 * (size_t)(G + 2), 8, ncclDouble, c->nccl, s) != ncclSuccess)
             st = QG_ERR_RCCL;
-        if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_set_halo_transport (status)");
+        if (st == QG_OK) st = comm_wait(c, s, nullptr, what);
         std::vector<double> sts(8 * (size_t)G);
         if (st == QG_OK &&
             hipMemcpy(sts.data(), hb + 8 * (size_t)(G + 2), sizeof(double) * sts.size(), hipMemcpyDeviceToHost) !=
@@ -562,18 +565,47 @@ int comm_set_peer(void *comm, int on, int64_t ld) {
         for (int r = 0; st == QG_OK && r < G; ++r)
             if (sts[8 * (size_t)r] != 0.0) {
                 if (r == c->rank || local == QG_OK)
-                    std::fprintf(stderr, "qg_mi355 rank %d/%d: peer-copy halo transport unavailable (rank %d: %s)\n",
-                                 c->rank, G, r, qg_strerror((int)sts[8 * (size_t)r]));
+                    std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: IPC regions unavailable (rank %d: %s)\n", c->rank,
+                                 G, what, r, qg_strerror((int)sts[8 * (size_t)r]));
                 st = QG_ERR_UNSUPPORTED;
                 break;
             }
     }
     if (hb) (void)hipFree(hb);
     (void)hipStreamDestroy(s);
-    if (st != QG_OK) {
-        peer_release(c);
-        return st;
+    if (st != QG_OK) region_release(g);
+    return st;
+}
+
+// Leave a peer transport: every rank drains its device, then one all-gather, so no
+// neighbour's writes can still be landing in a region when it is released.
+static int region_leave(Comm *c, Comm::IpcRegion &g, const char *what) {
+    QG_HIP(hipDeviceSynchronize());
+    const int b = comm_barrier(c, what);
+    region_release(g);
+    return b;
+}
+
+// Collective (every rank, same arguments): switch the halo rows of comm_halo_rows to the
+// peer-copy transport for rows of `ld` words, or back to RCCL (on = 0).  RCCL transport only:
+// the receive regions' IPC handles are all-gathered over it.
+int comm_set_peer(void *comm, int on, int64_t ld) {
+    Comm *c = static_cast<Comm *>(comm);
+    if (!c || c->failed) return QG_ERR_RCCL;
+    if (!on && !c->peer) return QG_OK;
+    if (on && !c->nccl) return QG_ERR_UNSUPPORTED;
+    if (on && ld < 1) return QG_ERR_INVALID_ARG;
+    if (on && c->peer && c->peer_ld == ld) return QG_OK;
+    if (c->peer) {
+        c->peer = false;
+        QG_CHECK(region_leave(c, c->halo_rx, "qg_comm_set_halo_transport (leave)"));
     }
+    if (!on) return QG_OK;
+    const int G = c->nranks;
+    std::vector<char> need((size_t)G, 0);
+    need[(size_t)((c->rank + 1) % G)] = need[(size_t)((c->rank - 1 + G) % G)] = 1;
+    QG_CHECK(region_create(c, c->halo_rx, sizeof(double) * (size_t)(PEER_HDR + 4 * PEER_ROWS * ld), need,
+                           "qg_comm_set_halo_transport"));
     c->peer = true;
     c->peer_ld = ld;
     c->pseq = 0;
@@ -591,8 +623,12 @@ static int peer_halo_rows(Comm *c, double *const *f2, int n2, int64_t ld, int64_
     if (ld != c->peer_ld) return QG_ERR_INVALID_ARG;
     const int64_t seq = ++c->pseq;
     const int par = (int)(seq & 1);
-    double *to_next = peer_region(c->prx_peer[0], ld, par, 0), *to_prev = peer_region(c->prx_peer[1], ld, par, 1);
-    const double *from_prev = peer_region(c->prx, ld, par, 0), *from_next = peer_region(c->prx, ld, par, 1);
+    const int G = c->nranks;
+    double *rx_next = c->halo_rx.remote[(size_t)((c->rank + 1) % G)];
+    double *rx_prev = c->halo_rx.remote[(size_t)((c->rank - 1 + G) % G)];
+    double *to_next = peer_region(rx_next, ld, par, 0), *to_prev = peer_region(rx_prev, ld, par, 1);
+    const double *from_prev = peer_region(c->halo_rx.local, ld, par, 0);
+    const double *from_next = peer_region(c->halo_rx.local, ld, par, 1);
     const size_t bytes = sizeof(double) * 2 * (size_t)ld;
     for (int f = 0; f < n2; ++f) {
         const double *b = f2[f];
@@ -603,14 +639,120 @@ static int peer_halo_rows(Comm *c, double *const *f2, int n2, int64_t ld, int64_
             rows_out[4 * f + 2 + q] = from_next + (2 * f + q) * ld;  // rows P, P+1
         }
     }
-    peer_signal_kernel<<<1, 64, 0, s>>>(reinterpret_cast<uint64_t *>(c->prx_peer[0]),
-                                        reinterpret_cast<uint64_t *>(c->prx_peer[1]) + 8, (uint64_t)seq);
+    peer_signal_kernel<<<1, 64, 0, s>>>(reinterpret_cast<uint64_t *>(rx_next), reinterpret_cast<uint64_t *>(rx_prev) + 8,
+                                        (uint64_t)seq);
     QG_LAUNCH_CHECK();
     const uint64_t limit = (uint64_t)(c->timeout_s * (double)c->clock_khz * 1000.0);
-    peer_wait_kernel<<<1, 64, 0, s>>>(reinterpret_cast<const uint64_t *>(c->prx), (uint64_t)seq, limit,
+    peer_wait_kernel<<<1, 64, 0, s>>>(reinterpret_cast<const uint64_t *>(c->halo_rx.local), (uint64_t)seq, limit,
                                       c->progress_d, c->seq + 1, c->perr_d);
     QG_LAUNCH_CHECK();
     ++c->seq;
+    return QG_OK;
+}
+
+// ---- peer record gather ----------------------------------------------------------------
+struct PgArgs {
+    const double *send;
+    double *recv;
+    int64_t count;
+    double *dst[PG_MAX_RANKS];  // the ranks' regions as mapped here
+    const double *mine;         // this rank's region
+    int G, rank, par;
+    uint64_t seq, limit;
+    int64_t *err;
+};
+
+// Workgroup (b, r): part b of this rank's record -> rank r's region (slot [par][rank]), r's flag
+// (rank, b) raised after every storing wave has drained (the release below writes the L2 back
+// at system scope); then wait for r's flag (r, b) here and copy r's part b into recv.  Every
+// workgroup stores before it waits, so no rank's kernel waits on a workgroup that is itself
+// waiting.  Double-buffered by gather parity: a rank's gather k + 2 starts only after its
+// gather k + 1 saw every peer's k + 1 flags, i.e. after every peer's gather k has finished.
+__global__ __launch_bounds__(256) void peer_gather_kernel(PgArgs a) {
+    const int b = blockIdx.x, r = blockIdx.y;
+    const int64_t hdr = (int64_t)a.G * PG_BLOCKS * 8;
+    const int64_t lo = a.count * b / PG_BLOCKS, hi = a.count * (b + 1) / PG_BLOCKS;
+    double *out = a.recv + (size_t)r * a.count;
+    if (r == a.rank) {
+        if (out != a.send)
+            for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = a.send[i];
+        return;
+    }
+    double *rem = a.dst[r] + hdr + ((size_t)a.par * a.G + a.rank) * a.count;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) rem[i] = a.send[i];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __shared__ int timed_out;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(a.dst[r]) + ((size_t)a.rank * PG_BLOCKS + b) * 8, a.seq,
+                           __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t *f = reinterpret_cast<const uint64_t *>(a.mine) + ((size_t)r * PG_BLOCKS + b) * 8;
+        const uint64_t t0 = wall_clock64();
+        timed_out = 0;
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
+            if (wall_clock64() - t0 > a.limit) {
+                __hip_atomic_store(a.err, (int64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                timed_out = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    if (timed_out) return;
+    const double *src = a.mine + hdr + ((size_t)a.par * a.G + r) * a.count;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) out[i] = src[i];
+}
+
+// Collective (every rank, same arguments): gather records of `count` doubles (the direct
+// solver's per-step rank records) by peer_gather_kernel, or by ncclAllGather (on = 0).
+int comm_set_peer_gather(void *comm, int on, int64_t count) {
+    Comm *c = static_cast<Comm *>(comm);
+    if (!c || c->failed) return QG_ERR_RCCL;
+    if (!on && !c->pgather) return QG_OK;
+    if (on && !c->nccl) return QG_ERR_UNSUPPORTED;
+    if (on && (count < 1 || c->nranks > PG_MAX_RANKS)) return QG_ERR_INVALID_ARG;
+    if (on && c->pgather && c->pg_count == count) return QG_OK;
+    if (c->pgather) {
+        c->pgather = false;
+        QG_CHECK(region_leave(c, c->gat_rx, "qg_comm_set_gather_transport (leave)"));
+    }
+    if (!on) return QG_OK;
+    const int G = c->nranks;
+    std::vector<char> need((size_t)G, 1);
+    QG_CHECK(region_create(c, c->gat_rx, sizeof(double) * (size_t)(G * PG_BLOCKS * 8 + 2 * (int64_t)G * count), need,
+                           "qg_comm_set_gather_transport"));
+    c->pgather = true;
+    c->pg_count = count;
+    c->gseq = 0;
+    return QG_OK;
+}
+
+// The solver's record all-gather: the peer kernel when selected, else comm_allgather.
+int comm_gather_records(void *user, const double *send, double *recv, int64_t count, hipStream_t s) {
+    Comm *c = static_cast<Comm *>(user);
+    if (!c || c->failed) return QG_ERR_RCCL;
+    if (!c->pgather) return comm_allgather(user, send, recv, count, s);
+    if (count != c->pg_count) return QG_ERR_INVALID_ARG;
+    if (c->nranks == 1) {  // (the one-rank ring's record is its own gather)
+        if (recv != send) QG_HIP(hipMemcpyAsync(recv, send, sizeof(double) * (size_t)count, hipMemcpyDeviceToDevice, s));
+        return QG_OK;
+    }
+    PgArgs a{};
+    a.send = send;
+    a.recv = recv;
+    a.count = count;
+    for (int r = 0; r < c->nranks; ++r) a.dst[r] = c->gat_rx.remote[(size_t)r];
+    a.mine = c->gat_rx.local;
+    a.G = c->nranks;
+    a.rank = c->rank;
+    a.seq = (uint64_t)++c->gseq;
+    a.par = (int)(a.seq & 1);
+    a.limit = (uint64_t)(c->timeout_s * (double)c->clock_khz * 1000.0);
+    a.err = c->perr_d;
+    peer_gather_kernel<<<dim3(PG_BLOCKS, (unsigned)c->nranks), 256, 0, s>>>(a);
+    QG_LAUNCH_CHECK();
     return QG_OK;
 }
 

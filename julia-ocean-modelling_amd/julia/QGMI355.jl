@@ -243,6 +243,13 @@ set_halo_transport!(s::QGState, peer::Bool) =
     @qgcheck qg_comm_set_halo_transport ccall((:qg_comm_set_halo_transport, libqg), Cint, (Ptr{Cvoid}, Cint),
                                               s.ctx, Cint(peer ? 1 : 0))
 
+"""`set_gather_transport!(s, peer)`: collective; `peer = true` gathers the direct solver's rank records
+with one kernel storing into every peer's IPC-mapped region (include/qg_mi355.h
+qg_comm_set_gather_transport)."""
+set_gather_transport!(s::QGState, peer::Bool) =
+    @qgcheck qg_comm_set_gather_transport ccall((:qg_comm_set_gather_transport, libqg), Cint, (Ptr{Cvoid}, Cint),
+                                                s.ctx, Cint(peer ? 1 : 0))
+
 """`run_model_no_output(model)` (run_model_no_output.jl:3-16) -> (zeta, psi) on the device,
 slots in the reference's order."""
 function run_model_no_output(model; kw...)

@@ -89,6 +89,7 @@ SIGNATURES = [
     ("qg_comm_set_timeout", C.c_int, [_vp, C.c_double]),
     ("qg_set_overlap", C.c_int, [_vp, C.c_int]),
     ("qg_comm_set_halo_transport", C.c_int, [_vp, C.c_int]),
+    ("qg_comm_set_gather_transport", C.c_int, [_vp, C.c_int]),
     ("qg_comm_probe", C.c_int, [_vp, C.c_int, C.POINTER(C.c_double)]),
     ("qg_set_pcg_sync", C.c_int, [_vp, C.c_int]),
     ("qg_pcg_certificate", C.c_int, [_vp, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64),

@@ -262,6 +262,16 @@ class State:
         call("qg_comm_set_halo_transport", self._ctx, modes[transport])
         self.halo_transport = transport
 
+    def set_gather_transport(self, transport="rccl"):
+        """qg_comm_set_gather_transport (collective, RCCL transport, direct solver): "rccl"
+        (ncclAllGather of the rank records) or "peer" (one kernel storing the record into every
+        peer's IPC-mapped region in parallel, flags, copy-out)."""
+        modes = {"rccl": 0, "peer": 1}
+        if transport not in modes:
+            raise ValueError(f"gather transport {transport!r}: one of {sorted(modes)}")
+        call("qg_comm_set_gather_transport", self._ctx, modes[transport])
+        self.gather_transport = transport
+
     def comm_probe(self, reps=20):
         """qg_comm_probe: event-timed halo exchange and record all-gather of one step, in
         isolation (every rank must call it): ms and bytes per collective."""

@@ -27,7 +27,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl"):
+def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl", gather="rccl"):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
@@ -56,6 +56,8 @@ def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl"
     st.comm_init(world, rank, bytes(uid.numpy().tobytes()))
     if halo != "rccl":
         st.set_halo_transport(halo)
+    if gather != "rccl":
+        st.set_gather_transport(gather)
     st.set_overlap(overlap)
     st.initialise()
     st.run(1, steps)
@@ -66,12 +68,12 @@ def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl"
     dist.destroy_process_group()
 
 
-def _run(world, M, P, steps, d, solver, overlap, halo="rccl"):
+def _run(world, M, P, steps, d, solver, overlap, halo="rccl", gather="rccl"):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap, halo))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap, halo, gather))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -125,19 +127,22 @@ def test_rccl_overlap_is_bit_identical():
             assert np.array_equal(a[r][n], b[r][n]), (r, n)
 
 
-@pytest.mark.parametrize("world,overlap", [(2, True), (4, True), (4, False)])
-def test_peer_halo_across_processes_bit_identical(world, overlap):
-    """The peer-copy halo transport between rank processes: each rank's receive region is
-    opened by its neighbours through IPC (here all on the one GPU), the rows arrive by copy
-    engine with an arrival flag; every slot of every slab bit for bit equal to the RCCL
-    send/recv transport (2 ranks: both neighbours are the same peer)."""
+@pytest.mark.parametrize("world,overlap,halo,gather", [(2, True, "peer", "rccl"), (4, True, "peer", "rccl"),
+                                                     (4, False, "peer", "rccl"), (2, True, "rccl", "peer"),
+                                                     (4, True, "peer", "peer"), (3, True, "peer", "peer")])
+def test_peer_transports_across_processes_bit_identical(world, overlap, halo, gather):
+    """The peer transports between rank processes: each rank's receive regions are opened by
+    the ranks that write into them through IPC (here all on the one GPU); halo rows arrive by
+    copy engine with an arrival flag, the solver's records by the one-kernel gather; every slot
+    of every slab bit for bit equal to the RCCL send/recv + ncclAllGather run (2 ranks: both
+    ring neighbours are the same peer)."""
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     with tempfile.TemporaryDirectory() as d0, tempfile.TemporaryDirectory() as d1:
-        a = _run(world, 64, 64, 6, d0, 0, overlap, "rccl")
-        b = _run(world, 64, 64, 6, d1, 0, overlap, "peer")
+        a = _run(world, 64, 48 * world // 2 if world == 3 else 64, 6, d0, 0, overlap)
+        b = _run(world, 64, 48 * world // 2 if world == 3 else 64, 6, d1, 0, overlap, halo, gather)
     for r in range(world):
         for n in ("zeta", "psi", "f_store"):
             assert np.array_equal(a[r][n], b[r][n]), (r, n)
