@@ -97,6 +97,9 @@ def parse():
                     help="RCCL transport, direct solver: how the per-step record all-gather travels "
                          "(qg_comm_set_gather_transport): rccl = ncclAllGather; peer = one kernel storing "
                          "into every peer's IPC-mapped region")
+    ap.add_argument("--no-transport-ab", dest="transport_ab", action="store_false", default=True,
+                    help="N > 1 (or --comm-self): skip re-timing the K steps with the other halo / gather "
+                         "transports (transport_ab)")
     ap.add_argument("--dropin-steps", type=int, default=20,
                     help="also time this many steps through the reference's own array signatures "
                          "(evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(...) on bare arrays, "
@@ -528,6 +531,44 @@ def main():
             comm = {"error": err or "failed on another rank"}
             overlap_ab = {"error": "skipped: the comm probe failed"}
 
+    # the same K steps with the other halo / gather transports (RCCL <-> peer copies), after the
+    # headline: a failure here (e.g. IPC unavailable between the GPUs) is reported, not fatal
+    transport_ab = None
+    if args.transport_ab and args.transport == "rccl" and (world > 1 or args.comm_self) \
+            and args.solver == "spectral" and args.comm_probe_reps > 0:
+        cur_h = getattr(st, "halo_transport", "rccl")
+        cur_g = getattr(st, "gather_transport", "rccl")
+        alt_h, alt_g = ("rccl", "rccl") if (cur_h, cur_g) == ("peer", "peer") else ("peer", "peer")
+        err3, el3 = None, None
+        try:
+            st.set_halo_transport(alt_h)
+            st.set_gather_transport(alt_g)
+            for _ in range(3):
+                st.step(t)
+                t += 1
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            st.run(t, K)
+            torch.cuda.synchronize()
+            el3 = time.perf_counter() - t1
+            t += K
+        except Exception as e:  # noqa: BLE001
+            err3 = f"{type(e).__name__}: {e}"
+        if all_ok(err3 is None):
+            if dist is not None:
+                tt = torch.tensor([el3], dtype=torch.float64, device=dev_red)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                el3 = float(tt.item())
+            transport_ab = {"halo_transport": alt_h, "gather_transport": alt_g, "value": world * K / el3,
+                            "ms_per_step": el3 * 1e3 / K, "steps": K, "halo_overlap": bool(args.overlap),
+                            "note": "the same K steps re-timed in this invocation with the halo and record-gather "
+                                    "transports switched (qg_comm_set_halo_transport / "
+                                    "qg_comm_set_gather_transport); the headline uses config's"}
+        else:
+            transport_ab = {"error": err3 or "failed on another rank"}
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -609,6 +650,8 @@ def main():
         out["comm"] = comm
     if overlap_ab is not None:
         out["overlap_ab"] = overlap_ab
+    if transport_ab is not None:
+        out["transport_ab"] = transport_ab
     if args.comm_probe_reps <= 0 and (world > 1 or args.comm_self) and args.solver == "spectral":
         out["comm"] = out["overlap_ab"] = {"skipped": "--comm-probe-reps 0"}
     if args.dropin_steps > 0 and world == 1 and args.solver == "spectral" and args.dtype == "f64" \

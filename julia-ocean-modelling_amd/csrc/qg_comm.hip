@@ -269,13 +269,6 @@ int comm_wait(void *comm, hipStream_t s, hipEvent_t ev, const char *what) {
     auto t_prog = t0;
     int64_t seen = c->progress_h ? __atomic_load_n(c->progress_h, __ATOMIC_RELAXED) : 0;
     for (long spin = 0;; ++spin) {
-        const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(s);
-        if (q == hipSuccess) return QG_OK;
-        if (q != hipErrorNotReady) {
-            std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: %s\n", c->rank, c->nranks, what, hipGetErrorString(q));
-            return QG_ERR_HIP;
-        }
-        const auto now = clk::now();
         if (c->perr_h && __atomic_load_n(c->perr_h, __ATOMIC_RELAXED) != 0) {
             std::fprintf(stderr,
                          "qg_mi355 rank %d/%d: %s: peer transfer #%lld did not arrive within %.1f s -- a peer "
@@ -287,6 +280,13 @@ int comm_wait(void *comm, hipStream_t s, hipEvent_t ev, const char *what) {
             c->failed = true;
             return QG_ERR_RCCL;
         }
+        const hipError_t q = ev ? hipEventQuery(ev) : hipStreamQuery(s);
+        if (q == hipSuccess) return QG_OK;
+        if (q != hipErrorNotReady) {
+            std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: %s\n", c->rank, c->nranks, what, hipGetErrorString(q));
+            return QG_ERR_HIP;
+        }
+        const auto now = clk::now();
         ncclResult_t ar = ncclSuccess;
         if (c->nccl && ncclCommGetAsyncError(c->nccl, &ar) == ncclSuccess && ar != ncclSuccess &&
             ar != ncclInProgress) {
@@ -471,8 +471,11 @@ __global__ void peer_wait_kernel(const uint64_t *flags, uint64_t seq, uint64_t l
         const uint64_t a = __hip_atomic_load(flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint64_t b = __hip_atomic_load(flags + 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         if (a >= seq && b >= seq) break;
-        if (wall_clock64() - t0 > limit) {
-            __hip_atomic_store(err, (int64_t)seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // (an earlier wait already timed out: the transport has failed, do not wait again)
+        if (wall_clock64() - t0 > limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+            int64_t zero = 0;
+            __hip_atomic_compare_exchange_strong(err, &zero, (int64_t)seq, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_SYSTEM);
             return;
         }
         __builtin_amdgcn_s_sleep(4);
@@ -621,6 +624,7 @@ static int peer_halo_rows(Comm *c, double *const *f2, int n2, int64_t ld, int64_
                           const double **rows_out) {
     if (n2 < 1 || 2 * n2 > PEER_ROWS) return QG_ERR_INVALID_ARG;
     if (ld != c->peer_ld) return QG_ERR_INVALID_ARG;
+    if (c->perr_h && __atomic_load_n(c->perr_h, __ATOMIC_RELAXED) != 0) return comm_wait(c, s, nullptr, "halo exchange");
     const int64_t seq = ++c->pseq;
     const int par = (int)(seq & 1);
     const int G = c->nranks;
@@ -691,8 +695,11 @@ __global__ __launch_bounds__(256) void peer_gather_kernel(PgArgs a) {
         const uint64_t t0 = wall_clock64();
         timed_out = 0;
         while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
-            if (wall_clock64() - t0 > a.limit) {
-                __hip_atomic_store(a.err, (int64_t)a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (wall_clock64() - t0 > a.limit ||
+                __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+                int64_t zero = 0;
+                __hip_atomic_compare_exchange_strong(a.err, &zero, (int64_t)a.seq, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM);
                 timed_out = 1;
                 break;
             }
@@ -735,6 +742,7 @@ int comm_gather_records(void *user, const double *send, double *recv, int64_t co
     if (!c || c->failed) return QG_ERR_RCCL;
     if (!c->pgather) return comm_allgather(user, send, recv, count, s);
     if (count != c->pg_count) return QG_ERR_INVALID_ARG;
+    if (c->perr_h && __atomic_load_n(c->perr_h, __ATOMIC_RELAXED) != 0) return comm_wait(c, s, nullptr, "record gather");
     if (c->nranks == 1) {  // (the one-rank ring's record is its own gather)
         if (recv != send) QG_HIP(hipMemcpyAsync(recv, send, sizeof(double) * (size_t)count, hipMemcpyDeviceToDevice, s));
         return QG_OK;
