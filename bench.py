@@ -89,10 +89,11 @@ def parse():
                          "interior rows' tendency runs (qg_set_overlap; bit-identical results; the default)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="N > 1 (or --comm-self): the exchange in stream order before the whole tendency")
-    ap.add_argument("--halo", choices=["rccl", "peer"], default="rccl",
+    ap.add_argument("--halo", choices=["rccl", "peer", "put"], default="rccl",
                     help="RCCL transport: how the halo rows travel (qg_comm_set_halo_transport): rccl = "
                          "pack + grouped send/recv; peer = copy-engine copies into the neighbours' "
-                         "IPC-mapped receive regions + arrival flags")
+                         "IPC-mapped receive regions + arrival flags; put = the same regions, rows stored "
+                         "by one small kernel")
     ap.add_argument("--gather", choices=["rccl", "peer"], default="rccl",
                     help="RCCL transport, direct solver: how the per-step record all-gather travels "
                          "(qg_comm_set_gather_transport): rccl = ncclAllGather; peer = one kernel storing "

@@ -266,9 +266,14 @@ int qg_set_overlap(qg_ctx *ctx, int on);
  * arrival flags and a one-lane kernel on the receiving side polls its own (bounded by the
  * comm timeout; a missing peer then fails the transport with QG_ERR_RCCL).  No collective
  * kernel holds compute units, so the exchange proceeds beside the interior tendency.
+ * QG_HALO_PUT: the same regions and flags, but the rows are stored by one small kernel
+ * (8 workgroups per direction, no LDS, few registers: it fits beside the interior tendency)
+ * whose workgroups also wait for the incoming parts -- one launch per exchange, fast in the
+ * serial schedule too.
  * QG_ERR_UNSUPPORTED (on every rank, the transport unchanged) when a rank cannot export or
- * open the regions.  The environment variable QG_HALO_PEER=1 selects it in qg_comm_init. */
-enum { QG_HALO_RCCL = 0, QG_HALO_PEER = 1 };
+ * open the regions.  The environment variable QG_HALO_PEER=1 (2: QG_HALO_PUT) selects it in
+ * qg_comm_init. */
+enum { QG_HALO_RCCL = 0, QG_HALO_PEER = 1, QG_HALO_PUT = 2 };
 int qg_comm_set_halo_transport(qg_ctx *ctx, int transport);
 /* How the direct solver's per-step record all-gather travels (collective, RCCL transport
  * only, spectral solver only: QG_ERR_UNSUPPORTED for PCG).

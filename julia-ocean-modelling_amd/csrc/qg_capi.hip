@@ -953,7 +953,7 @@ int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
     QG_CHECK(comm_init(&c->comm, nranks, rank, id));
     QG_CHECK(comm_attach(c, nranks, rank));
     if (const char *e = std::getenv("QG_HALO_PEER"))  // (every rank sees the same environment)
-        if (std::atoi(e) != 0) QG_CHECK(qg_comm_set_halo_transport(c, QG_HALO_PEER));
+        if (std::atoi(e) != 0) QG_CHECK(qg_comm_set_halo_transport(c, std::atoi(e) == 2 ? QG_HALO_PUT : QG_HALO_PEER));
     if (const char *e = std::getenv("QG_GATHER_PEER"))
         if (std::atoi(e) != 0 && c->spec) QG_CHECK(qg_comm_set_gather_transport(c, QG_GATHER_PEER));
     return QG_OK;
@@ -968,10 +968,11 @@ int qg_comm_set_gather_transport(qg_ctx *c, int transport) {
 }
 
 int qg_comm_set_halo_transport(qg_ctx *c, int transport) {
-    if (!c || (transport != QG_HALO_RCCL && transport != QG_HALO_PEER)) return QG_ERR_INVALID_ARG;
+    if (!c || (transport != QG_HALO_RCCL && transport != QG_HALO_PEER && transport != QG_HALO_PUT))
+        return QG_ERR_INVALID_ARG;
     if (!c->distributed || !c->comm) return QG_ERR_RCCL;
     QG_HIP(hipSetDevice(c->device));
-    return comm_set_peer(c->comm, transport == QG_HALO_PEER, c->row_words());
+    return comm_set_peer(c->comm, transport == QG_HALO_RCCL ? 0 : transport == QG_HALO_PEER ? 1 : 2, c->row_words());
 }
 
 int qg_comm_init_host(qg_ctx *c, int nranks, int rank, qg_allgather_fn allgather, qg_sendrecv_fn sendrecv,

@@ -54,6 +54,7 @@ struct Comm {
     };
     IpcRegion halo_rx, gat_rx;
     bool peer = false;
+    bool put = false;  // halo by the put kernel (QG_HALO_PUT) instead of the copy engine
     int64_t peer_ld = 0;
     int64_t pseq = 0;  // peer halo exchanges posted (the arrival flags' values)
     bool pgather = false;
@@ -64,7 +65,10 @@ struct Comm {
 };
 
 constexpr int PEER_ROWS = 8;       // rows per direction (4 fields x 2)
-constexpr int64_t PEER_HDR = 16;   // words before the rows: flag from_prev @0, from_next @8
+constexpr int PUT_BLOCKS = 8;      // halo put kernel: workgroups per direction
+// words before the rows: flags (dir, part) at (dir * PUT_BLOCKS + part) * 8 (dir 0 = from_prev,
+// 1 = from_next; the copy-engine mode uses part 0)
+constexpr int64_t PEER_HDR = 2 * PUT_BLOCKS * 8;
 constexpr int PG_BLOCKS = 4;       // record gather: workgroups per peer
 constexpr int PG_MAX_RANKS = 64;
 
@@ -469,7 +473,7 @@ __global__ void peer_wait_kernel(const uint64_t *flags, uint64_t seq, uint64_t l
     const uint64_t t0 = wall_clock64();
     for (;;) {
         const uint64_t a = __hip_atomic_load(flags, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        const uint64_t b = __hip_atomic_load(flags + 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t b = __hip_atomic_load(flags + PUT_BLOCKS * 8, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         if (a >= seq && b >= seq) break;
         // (an earlier wait already timed out: the transport has failed, do not wait again)
         if (wall_clock64() - t0 > limit || __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
@@ -589,6 +593,54 @@ static int region_leave(Comm *c, Comm::IpcRegion &g, const char *what) {
     return b;
 }
 
+// Halo by kernel (QG_HALO_PUT): workgroup (b, d) stores part b of this rank's outgoing rows of
+// direction d (0: top rows -> next's from_prev, 1: bottom rows -> prev's from_next) into the
+// neighbour's region, drains its stores, releases at system scope and raises the neighbour's
+// flag (d, b); then it waits for this rank's own flag (d, b), raised by the neighbour's
+// matching workgroup.  Every workgroup stores before it waits.  A few small workgroups (no
+// LDS, few registers) that fit beside the interior tendency; one launch per exchange.
+struct PutArgs {
+    const double *src[2][4];  // [dir][field]: the field's two outgoing rows (contiguous)
+    double *dst[2];           // the neighbours' rows of this exchange's parity
+    uint64_t *flag[2];        // the neighbours' flag bases for this direction
+    const uint64_t *mine;     // this rank's flags
+    int64_t words, seg;       // words per direction; words per field (2 rows)
+    uint64_t seq, limit;
+    int64_t *err, *progress;
+    int64_t prog;
+};
+
+__global__ __launch_bounds__(256) void halo_put_kernel(PutArgs a) {
+    const int b = blockIdx.x, d = blockIdx.y;
+    const int64_t lo = a.words * b / PUT_BLOCKS, hi = a.words * (b + 1) / PUT_BLOCKS;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+        const int64_t f = i / a.seg;
+        a.dst[d][i] = a.src[d][f][i - f * a.seg];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(a.flag[d] + (size_t)b * 8, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t *f = a.mine + ((size_t)d * PUT_BLOCKS + b) * 8;
+        const uint64_t t0 = wall_clock64();
+        bool ok = true;
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < a.seq) {
+            if (wall_clock64() - t0 > a.limit ||
+                __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) {
+                int64_t zero = 0;
+                __hip_atomic_compare_exchange_strong(a.err, &zero, (int64_t)a.seq, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (ok && b == 0 && d == 0 && a.progress)
+            __hip_atomic_store(a.progress, a.prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // Collective (every rank, same arguments): switch the halo rows of comm_halo_rows to the
 // peer-copy transport for rows of `ld` words, or back to RCCL (on = 0).  RCCL transport only:
 // the receive regions' IPC handles are all-gathered over it.
@@ -598,7 +650,11 @@ int comm_set_peer(void *comm, int on, int64_t ld) {
     if (!on && !c->peer) return QG_OK;
     if (on && !c->nccl) return QG_ERR_UNSUPPORTED;
     if (on && ld < 1) return QG_ERR_INVALID_ARG;
-    if (on && c->peer && c->peer_ld == ld) return QG_OK;
+    if (on && c->peer && c->peer_ld == ld) {  // (same regions; only the mover changes)
+        QG_HIP(hipDeviceSynchronize());
+        c->put = on == 2;
+        return comm_barrier(c, "qg_comm_set_halo_transport (mode)");
+    }
     if (c->peer) {
         c->peer = false;
         QG_CHECK(region_leave(c, c->halo_rx, "qg_comm_set_halo_transport (leave)"));
@@ -610,6 +666,7 @@ int comm_set_peer(void *comm, int on, int64_t ld) {
     QG_CHECK(region_create(c, c->halo_rx, sizeof(double) * (size_t)(PEER_HDR + 4 * PEER_ROWS * ld), need,
                            "qg_comm_set_halo_transport"));
     c->peer = true;
+    c->put = on == 2;
     c->peer_ld = ld;
     c->pseq = 0;
     return QG_OK;
@@ -634,6 +691,33 @@ static int peer_halo_rows(Comm *c, double *const *f2, int n2, int64_t ld, int64_
     const double *from_prev = peer_region(c->halo_rx.local, ld, par, 0);
     const double *from_next = peer_region(c->halo_rx.local, ld, par, 1);
     const size_t bytes = sizeof(double) * 2 * (size_t)ld;
+    if (c->put) {
+        PutArgs a{};
+        for (int f = 0; f < n2; ++f) {
+            a.src[0][f] = f2[f] + fidx(0, P - 1, ld);
+            a.src[1][f] = f2[f] + fidx(0, 1, ld);
+            for (int q = 0; q < 2; ++q) {
+                rows_out[4 * f + q] = from_prev + (2 * f + q) * ld;
+                rows_out[4 * f + 2 + q] = from_next + (2 * f + q) * ld;
+            }
+        }
+        a.dst[0] = to_next;
+        a.dst[1] = to_prev;
+        a.flag[0] = reinterpret_cast<uint64_t *>(rx_next);                        // next's (0, b)
+        a.flag[1] = reinterpret_cast<uint64_t *>(rx_prev) + PUT_BLOCKS * 8;       // prev's (1, b)
+        a.mine = reinterpret_cast<const uint64_t *>(c->halo_rx.local);
+        a.words = 2 * (int64_t)n2 * ld;
+        a.seg = 2 * ld;
+        a.seq = (uint64_t)seq;
+        a.limit = (uint64_t)(c->timeout_s * (double)c->clock_khz * 1000.0);
+        a.err = c->perr_d;
+        a.progress = c->progress_d;
+        a.prog = c->seq + 1;
+        halo_put_kernel<<<dim3(PUT_BLOCKS, 2), 256, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        ++c->seq;
+        return QG_OK;
+    }
     for (int f = 0; f < n2; ++f) {
         const double *b = f2[f];
         QG_HIP(hipMemcpyAsync(to_next + 2 * f * ld, b + fidx(0, P - 1, ld), bytes, hipMemcpyDeviceToDeviceNoCU, s));
@@ -643,7 +727,8 @@ static int peer_halo_rows(Comm *c, double *const *f2, int n2, int64_t ld, int64_
             rows_out[4 * f + 2 + q] = from_next + (2 * f + q) * ld;  // rows P, P+1
         }
     }
-    peer_signal_kernel<<<1, 64, 0, s>>>(reinterpret_cast<uint64_t *>(rx_next), reinterpret_cast<uint64_t *>(rx_prev) + 8,
+    peer_signal_kernel<<<1, 64, 0, s>>>(reinterpret_cast<uint64_t *>(rx_next),
+                                        reinterpret_cast<uint64_t *>(rx_prev) + PUT_BLOCKS * 8,
                                         (uint64_t)seq);
     QG_LAUNCH_CHECK();
     const uint64_t limit = (uint64_t)(c->timeout_s * (double)c->clock_khz * 1000.0);

@@ -254,9 +254,10 @@ class State:
 
     def set_halo_transport(self, transport="rccl"):
         """qg_comm_set_halo_transport (collective, RCCL transport only): "rccl" (pack kernel +
-        grouped send/recv) or "peer" (copy-engine copies into the neighbours' IPC-mapped
-        receive regions + arrival flags; no collective kernel beside the interior tendency)."""
-        modes = {"rccl": 0, "peer": 1}
+        grouped send/recv), "peer" (copy-engine copies into the neighbours' IPC-mapped
+        receive regions + arrival flags; no collective kernel beside the interior tendency) or
+        "put" (the same regions, rows stored by one small kernel that also waits)."""
+        modes = {"rccl": 0, "peer": 1, "put": 2}
         if transport not in modes:
             raise ValueError(f"halo transport {transport!r}: one of {sorted(modes)}")
         call("qg_comm_set_halo_transport", self._ctx, modes[transport])

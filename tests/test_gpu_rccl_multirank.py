@@ -129,7 +129,8 @@ def test_rccl_overlap_is_bit_identical():
 
 @pytest.mark.parametrize("world,overlap,halo,gather", [(2, True, "peer", "rccl"), (4, True, "peer", "rccl"),
                                                      (4, False, "peer", "rccl"), (2, True, "rccl", "peer"),
-                                                     (4, True, "peer", "peer"), (3, True, "peer", "peer")])
+                                                     (4, True, "peer", "peer"), (3, True, "peer", "peer"),
+                                                     (4, True, "put", "peer"), (2, False, "put", "rccl")])
 def test_peer_transports_across_processes_bit_identical(world, overlap, halo, gather):
     """The peer transports between rank processes: each rank's receive regions are opened by
     the ranks that write into them through IPC (here all on the one GPU); halo rows arrive by

@@ -56,9 +56,11 @@ def _ring_state(qgamd, m, transport, overlap, **kw):
     return st
 
 
-@pytest.mark.parametrize("M,P,f32,overlap", [(64, 48, False, True), (64, 48, False, False), (96, 64, True, True),
-                                             (1024, 256, False, True)])
-def test_one_rank_peer_halo_bit_identical(M, P, f32, overlap):
+@pytest.mark.parametrize("M,P,f32,overlap,halo", [(64, 48, False, True, "peer"), (64, 48, False, False, "peer"),
+                                                  (96, 64, True, True, "peer"), (1024, 256, False, True, "peer"),
+                                                  (64, 48, False, True, "put"), (64, 48, False, False, "put"),
+                                                  (96, 64, True, True, "put"), (1024, 256, False, True, "put")])
+def test_one_rank_peer_halo_bit_identical(M, P, f32, overlap, halo):
     """The peer-copy halo transport (copy engine into the IPC-style receive region, arrival
     flags, one-lane wait kernel) over the one-rank ring: every slot bit for bit equal to the
     RCCL send/recv transport, for both schedules and both precisions."""
@@ -72,7 +74,7 @@ def test_one_rank_peer_halo_bit_identical(M, P, f32, overlap):
     kw = {"dtype": torch.float32} if f32 else {}
     a = _ring_state(qgamd, m, "rccl", overlap, **kw)
     a.run(1, 9)
-    b = _ring_state(qgamd, m, "peer", overlap, **kw)
+    b = _ring_state(qgamd, m, halo, overlap, **kw)
     b.run(1, 9)
     torch.cuda.synchronize()
     for n in ("zeta", "psi", "f_store"):
@@ -100,8 +102,10 @@ def test_one_rank_peer_halo_switch_and_probe():
     b.run(5, 4)
     b.set_halo_transport("rccl")
     b.run(9, 2)
+    b.set_halo_transport("put")
+    b.run(11, 1)
     b.set_halo_transport("peer")
-    b.run(11, 2)
+    b.run(12, 1)
     torch.cuda.synchronize()
     for n in ("zeta", "psi", "f_store"):
         assert np.array_equal(a.to_numpy(n), b.to_numpy(n)), n
