@@ -7,6 +7,7 @@ cd $R || exit 1
 O=gpurun_out/r04v
 mkdir -p $O
 export QG_COMM_TIMEOUT=20
+export QG_VERIFY_PUT=1
 timeout -k 10 700 python -u -m pytest -x -v -p no:cacheprovider --timeout 200 --timeout-method thread \
   tests/test_gpu_rccl_ring.py "tests/test_gpu_rccl_multirank.py::test_peer_transports_across_processes_bit_identical" \
   "tests/test_gpu_rccl_multirank.py::test_rccl_silent_peer_returns_rccl_error" > $O/tests.log 2>&1
