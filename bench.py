@@ -385,6 +385,8 @@ def main():
             and args.solver == "spectral":
         st.set_gather_transport(args.gather)
     st.set_overlap(args.overlap)
+    cur_halo = getattr(st, "halo_transport", "rccl")
+    cur_gather = getattr(st, "gather_transport", "rccl")
     st.initialise()
     torch.cuda.synchronize()
     setup_ms = (time.perf_counter() - t_setup) * 1e3
@@ -537,13 +539,16 @@ def main():
     transport_ab = None
     if args.transport_ab and args.transport == "rccl" and (world > 1 or args.comm_self) \
             and args.solver == "spectral" and args.comm_probe_reps > 0:
-        cur_h = getattr(st, "halo_transport", "rccl")
-        cur_g = getattr(st, "gather_transport", "rccl")
-        alt_h, alt_g = ("rccl", "rccl") if (cur_h, cur_g) == ("peer", "peer") else ("peer", "peer")
+        # RCCL headline -> the peer transports in their best measured schedule (put halo +
+        # peer gather, overlap off: the 10 us put beats splitting the tendency, r04v); a peer
+        # headline -> RCCL with the overlap on
+        peer_now = (cur_halo, cur_gather) != ("rccl", "rccl")
+        alt_h, alt_g, alt_ov = ("rccl", "rccl", True) if peer_now else ("put", "peer", False)
         err3, el3 = None, None
         try:
             st.set_halo_transport(alt_h)
             st.set_gather_transport(alt_g)
+            st.set_overlap(alt_ov)
             for _ in range(3):
                 st.step(t)
                 t += 1
@@ -563,10 +568,10 @@ def main():
                 dist.all_reduce(tt, op=dist.ReduceOp.MAX)
                 el3 = float(tt.item())
             transport_ab = {"halo_transport": alt_h, "gather_transport": alt_g, "value": world * K / el3,
-                            "ms_per_step": el3 * 1e3 / K, "steps": K, "halo_overlap": bool(args.overlap),
+                            "ms_per_step": el3 * 1e3 / K, "steps": K, "halo_overlap": alt_ov,
                             "note": "the same K steps re-timed in this invocation with the halo and record-gather "
-                                    "transports switched (qg_comm_set_halo_transport / "
-                                    "qg_comm_set_gather_transport); the headline uses config's"}
+                                    "transports (and the overlap) switched (qg_comm_set_halo_transport / "
+                                    "qg_comm_set_gather_transport / qg_set_overlap); the headline uses config's"}
         else:
             transport_ab = {"error": err3 or "failed on another rank"}
 
@@ -622,10 +627,9 @@ def main():
                            "not xGMI, not a measurement)" if one_gpu else args.transport)
                           if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
             "halo_overlap": bool(args.overlap and (world > 1 or args.comm_self)),
-            "halo_transport": (getattr(st, "halo_transport", "rccl") if args.transport == "rccl"
-                               and (world > 1 or args.comm_self) else None),
-            "gather_transport": (getattr(st, "gather_transport", "rccl") if args.transport == "rccl"
-                                 and (world > 1 or args.comm_self) and args.solver == "spectral" else None),
+            "halo_transport": (cur_halo if args.transport == "rccl" and (world > 1 or args.comm_self) else None),
+            "gather_transport": (cur_gather if args.transport == "rccl" and (world > 1 or args.comm_self)
+                                 and args.solver == "spectral" else None),
         },
         "roofline": {
             "bound": "hbm",

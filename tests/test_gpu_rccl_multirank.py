@@ -141,8 +141,6 @@ def test_peer_transports_across_processes_bit_identical(world, overlap, halo, ga
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    if halo == "put" and not os.environ.get("QG_VERIFY_PUT"):
-        pytest.skip("put mode awaiting its first GPU run (QG_VERIFY_PUT=1)")
     with tempfile.TemporaryDirectory() as d0, tempfile.TemporaryDirectory() as d1:
         a = _run(world, 64, 48 * world // 2 if world == 3 else 64, 6, d0, 0, overlap)
         b = _run(world, 64, 48 * world // 2 if world == 3 else 64, 6, d1, 0, overlap, halo, gather)
@@ -307,8 +305,6 @@ def test_rccl_silent_peer_returns_rccl_error(halo):
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    if halo != "rccl" and not os.environ.get("QG_VERIFY_PUT"):
-        pytest.skip("peer fail-fast awaiting its first GPU run (QG_VERIFY_PUT=1)")
     from qgamd import _lib
 
     with tempfile.TemporaryDirectory() as d:

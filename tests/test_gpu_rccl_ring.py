@@ -71,8 +71,6 @@ def test_one_rank_peer_halo_bit_identical(M, P, f32, overlap, halo):
         pytest.skip("no GPU")
     import qgamd
 
-    if halo == "put" and not os.environ.get("QG_VERIFY_PUT"):
-        pytest.skip("put mode awaiting its first GPU run (QG_VERIFY_PUT=1)")
     m = qgamd.bench_model(M, P=P)
     kw = {"dtype": torch.float32} if f32 else {}
     a = _ring_state(qgamd, m, "rccl", overlap, **kw)
@@ -105,7 +103,7 @@ def test_one_rank_peer_halo_switch_and_probe():
     b.run(5, 4)
     b.set_halo_transport("rccl")
     b.run(9, 2)
-    b.set_halo_transport("put" if os.environ.get("QG_VERIFY_PUT") else "peer")
+    b.set_halo_transport("put")
     b.run(11, 1)
     b.set_halo_transport("peer")
     b.run(12, 1)
