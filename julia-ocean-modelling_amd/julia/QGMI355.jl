@@ -237,11 +237,15 @@ tendency runs (bit-identical; include/qg_mi355.h qg_set_overlap)."""
 set_overlap!(s::QGState, on::Bool=true) =
     @qgcheck qg_set_overlap ccall((:qg_set_overlap, libqg), Cint, (Ptr{Cvoid}, Cint), s.ctx, Cint(on))
 
-"""`set_halo_transport!(s, peer)`: collective; `peer = true` sends the halo rows by copy engine into
-the neighbours' IPC-mapped receive regions (include/qg_mi355.h qg_comm_set_halo_transport)."""
-set_halo_transport!(s::QGState, peer::Bool) =
+"""`set_halo_transport!(s, mode)`: collective; `mode` = `:rccl` (send/recv), `:peer` (copy engine into the
+neighbours' IPC-mapped regions) or `:put` (one small kernel storing into them) -- include/qg_mi355.h
+qg_comm_set_halo_transport."""
+function set_halo_transport!(s::QGState, mode::Symbol)
+    code = mode === :rccl ? 0 : mode === :peer ? 1 : mode === :put ? 2 :
+           throw(ArgumentError("halo transport $mode: one of :rccl, :peer, :put"))
     @qgcheck qg_comm_set_halo_transport ccall((:qg_comm_set_halo_transport, libqg), Cint, (Ptr{Cvoid}, Cint),
-                                              s.ctx, Cint(peer ? 1 : 0))
+                                              s.ctx, Cint(code))
+end
 
 """`set_gather_transport!(s, peer)`: collective; `peer = true` gathers the direct solver's rank records
 with one kernel storing into every peer's IPC-mapped region (include/qg_mi355.h
