@@ -545,7 +545,10 @@ def main():
         peer_now = (cur_halo, cur_gather) != ("rccl", "rccl")
         alt_h, alt_g, alt_ov = ("rccl", "rccl", True) if peer_now else ("put", "peer", False)
         err3, el3 = None, None
+        import ctypes as C
         try:
+            # (a peer that never answers fails this leg within 20 s, not the default 120 s)
+            qgamd._lib.call("qg_comm_set_timeout", st._ctx, C.c_double(20.0))
             st.set_halo_transport(alt_h)
             st.set_gather_transport(alt_g)
             st.set_overlap(alt_ov)
