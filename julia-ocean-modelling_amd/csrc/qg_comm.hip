@@ -642,8 +642,9 @@ __global__ __launch_bounds__(256) void halo_put_kernel(PutArgs a) {
 }
 
 // Collective (every rank, same arguments): switch the halo rows of comm_halo_rows to the
-// peer-copy transport for rows of `ld` words, or back to RCCL (on = 0).  RCCL transport only:
-// the receive regions' IPC handles are all-gathered over it.
+// peer transport for rows of `ld` words -- on = 1: copy engine, on = 2: put kernel (the same
+// regions and flags; a switch between the two keeps them, flag values stay monotonic) -- or
+// back to RCCL (on = 0).  RCCL transport only: the regions' IPC handles are all-gathered over it.
 int comm_set_peer(void *comm, int on, int64_t ld) {
     Comm *c = static_cast<Comm *>(comm);
     if (!c || c->failed) return QG_ERR_RCCL;
