@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define QG_ABI_VERSION 4
+#define QG_ABI_VERSION 5
 
 typedef enum {
     QG_OK = 0,
@@ -158,7 +158,8 @@ int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2
  * above after every call, slots 2-3 of zeta and psi NOT maintained -- the reference never
  * reads them (only evolve_zeta_layer! reads f_store's history), so its loop computes the
  * same values: no shifts of zeta and psi, the new zeta written to slot 2 and copied to slot 1
- * (one slot copy per step instead of four).                                                  */
+ * (one slot copy per step instead of four).  Switching from QG_KEEP_ORDER_SLOT1 straight to
+ * on = 1 returns QG_ERR_INVALID_ARG (slots 2-3 of zeta and psi hold stale values then).      */
 #define QG_KEEP_ORDER_SLOT1 2
 int qg_set_keep_order(qg_ctx *ctx, int on);
 int qg_get_stats(qg_ctx *ctx, qg_stats *out);
@@ -172,7 +173,7 @@ int qg_get_stats(qg_ctx *ctx, qg_stats *out);
  * within two polling intervals (the latch is copied to the host every QG_PACE_STEPS solves and
  * read one interval later, waiting for that copy if needed: the host stays at most two
  * intervals ahead, so every rank stops at the same step, graph replays included), by the end of qg_run (it settles and reads the
- * latch), by qg_synchronize, and in qg_pcg_certificate's record.  sync = 1 (or QG_PCG_SYNC=1 at create): the host reads every
+ * latch), by qg_synchronize, and in qg_pcg_certificate's record.  sync = 1: the host reads every
  * residual and runs the general PCG iteration when the certificate fails (the old form).  */
 int qg_set_pcg_sync(qg_ctx *ctx, int sync);
 /* deferred certificates so far: solves certified, failures, first failing solve (1-based,
@@ -316,6 +317,32 @@ int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], con
 /* the `factor \ b` of sp_solve_* (laplacian.jl:78-111) / model.jl:186,191 */
 int qg_solver_solve(qg_solver *s, const double *f_1, const double *f_2, double *out_1, double *out_2);
 int qg_solver_destroy(qg_solver *s);
+
+/* ---- kernel-form selection (process-wide) ---------------------------------------------
+ * Every kernel's form is chosen by problem size.  qg_set_form forces one form, for the tests
+ * that check the alternative forms against each other and for BASELINE config 3's LDS tile
+ * sweep; value 0 restores the automatic choice (the default).  Read at every launch
+ * (QG_FORM_PCG_NO_CERTIFICATE: when a context's PCG solver is built, i.e. qg_create /
+ * qg_comm_init).  qg_get_form returns the current value (or QG_ERR_INVALID_ARG).            */
+enum {
+    QG_FORM_TENDENCY = 0,           /* QG_TEND_* below                                       */
+    QG_FORM_TENDENCY_TILE = 1,      /* (W << 16) | R: the LDS-ring tendency in strips W points  *
+                                     * wide (W in 64, 128, 256, 512), about R rows per          *
+                                     * workgroup (config 3's tile sweep)                        */
+    QG_FORM_ROW_SPLIT = 2,          /* 1: row lengths that are not powers of two take the split *
+                                     * pipeline (row transforms and y-recurrences as separate   *
+                                     * kernels) at every M, not only above 3200 points          */
+    QG_FORM_PCG_NO_CERTIFICATE = 3, /* 1: PCG never takes the one-step certificate; it runs the *
+                                     * alpha iteration (z0 = M^-1 b, alpha = (b,z0)/(z0,B z0),  *
+                                     * then CG) that non-invertible back-projections need       */
+    QG_FORM_COUNT = 4
+};
+enum { QG_TEND_AUTO = 0, QG_TEND_RING = 1, QG_TEND_DIRECT = 2, QG_TEND_ONE_POINT = 3 };
+/* QG_TEND_RING: the LDS-ring kernel at every size; QG_TEND_DIRECT: the cache-resident one-point
+ * kernel at every size; QG_TEND_ONE_POINT: Float32 states use the one-point kernels instead of
+ * the two-points-per-thread pair kernel (size rule otherwise).  All forms are bit-identical. */
+int qg_set_form(int which, int value);
+int qg_get_form(int which);
 
 /* ---- stateless kernels on (M+2, P+2) device fields (ghost ring refreshed on output) ---- */
 int qg_laplace_5p(const double *u, double *out, int64_t M, int64_t P, double dx, void *stream); /* laplacian.jl:15-27 */

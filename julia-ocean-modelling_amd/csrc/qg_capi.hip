@@ -1,6 +1,7 @@
 // C-ABI implementation (include/qg_mi355.h): model context, slot rotation, solver handles,
 // stateless operators.  Everything is enqueued on the caller's stream; nothing in a step
 // allocates, synchronises or touches the host.
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -14,6 +15,8 @@
 #include "qg_spectral.hpp"
 
 namespace qg {
+static std::atomic<int> g_form[QG_FORM_COUNT];  // qg_set_form (zero-initialised: automatic)
+int form(int which) { return which >= 0 && which < QG_FORM_COUNT ? g_form[which].load(std::memory_order_relaxed) : 0; }
 int comm_destroy(void *comm);
 int comm_allgather(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
 int comm_halo(void *comm, double *const *fields, int nfields, int64_t M, int64_t P, int depth, double *halo_buf,
@@ -93,7 +96,6 @@ struct qg_ctx {
     // which the reference never reads, are not maintained (no shifts of zeta and psi; the new
     // zeta goes through slot 2, one slot copy)
     int keep_order = 0;
-    bool no_fshift_fuse = std::getenv("QG_NO_FSHIFT_FUSE") != nullptr;  // (A/B: the separate shift)
     bool capturing = false;  // a step graph is being captured (no host reads, no polls)
     // deferred PCG: the latch is copied to page-locked memory every QG_PACE_STEPS steps and
     // read one interval later without blocking, so a failed certificate stops qg_step /
@@ -124,6 +126,23 @@ struct qg_ctx {
 extern "C" {
 
 int qg_abi_version(void) { return QG_ABI_VERSION; }
+
+int qg_set_form(int which, int value) {
+    if (which < 0 || which >= QG_FORM_COUNT || value < 0) return QG_ERR_INVALID_ARG;
+    if (which == QG_FORM_TENDENCY && value > QG_TEND_ONE_POINT) return QG_ERR_INVALID_ARG;
+    if ((which == QG_FORM_ROW_SPLIT || which == QG_FORM_PCG_NO_CERTIFICATE) && value > 1) return QG_ERR_INVALID_ARG;
+    if (which == QG_FORM_TENDENCY_TILE && value != 0) {
+        const int w = value >> 16, r = value & 0xffff;
+        if ((w != 64 && w != 128 && w != 256 && w != 512) || r < 1) return QG_ERR_INVALID_ARG;
+    }
+    qg::g_form[which].store(value, std::memory_order_relaxed);
+    return QG_OK;
+}
+
+int qg_get_form(int which) {
+    if (which < 0 || which >= QG_FORM_COUNT) return QG_ERR_INVALID_ARG;
+    return qg::form(which);
+}
 
 const char *qg_strerror(int s) {
     switch (s) {
@@ -378,7 +397,7 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     // F(t-2) at every point anyway and writes them one slot down after reading, fshift1/2), so
     // only zeta is shifted here -- zeta's slot 1 is read with a stencil and cannot be
     // overwritten in place
-    const bool fuse_fshift = c->keep_order && !c->distributed && timestep >= 3 && !c->no_fshift_fuse;
+    const bool fuse_fshift = c->keep_order && !c->distributed && timestep >= 3;
     const bool lean = c->keep_order == QG_KEEP_ORDER_SLOT1;
     if (c->keep_order && !lean) {
         void *arr[2] = {c->zeta, c->fst};
@@ -722,6 +741,9 @@ int qg_canonicalize(qg_ctx *c) {
 
 int qg_set_keep_order(qg_ctx *c, int on) {
     if (!c || on < 0 || on > QG_KEEP_ORDER_SLOT1) return QG_ERR_INVALID_ARG;
+    // slots 2-3 of zeta and psi were not maintained in the lean mode: full keep-order could
+    // not keep its promise for the next two calls
+    if (on == 1 && c->keep_order == QG_KEEP_ORDER_SLOT1) return QG_ERR_INVALID_ARG;
     if (on && !c->keep_order && c->zeta) QG_CHECK(qg_canonicalize(c));
     if (c->keep_order != on) drop_graphs(c);
     c->keep_order = on;
@@ -952,10 +974,26 @@ int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
     }
     QG_CHECK(comm_init(&c->comm, nranks, rank, id));
     QG_CHECK(comm_attach(c, nranks, rank));
-    if (const char *e = std::getenv("QG_HALO_PEER"))  // (every rank sees the same environment)
-        if (std::atoi(e) != 0) QG_CHECK(qg_comm_set_halo_transport(c, std::atoi(e) == 2 ? QG_HALO_PUT : QG_HALO_PEER));
+    // environment opt-ins of the peer transports (every rank sees the same environment).  A
+    // node whose ranks cannot share the IPC regions (QG_ERR_UNSUPPORTED, the same verdict on
+    // every rank) keeps the RCCL transport: the communicator attached above works, so the
+    // init succeeds; only the explicit qg_comm_set_*_transport calls report the refusal.
+    if (const char *e = std::getenv("QG_HALO_PEER"))
+        if (std::atoi(e) != 0) {
+            const int st = qg_comm_set_halo_transport(c, std::atoi(e) == 2 ? QG_HALO_PUT : QG_HALO_PEER);
+            if (st == QG_ERR_UNSUPPORTED)
+                std::fprintf(stderr, "qg_mi355: rank %d: QG_HALO_PEER: peer regions unavailable, the halo stays on RCCL\n", rank);
+            else
+                QG_CHECK(st);
+        }
     if (const char *e = std::getenv("QG_GATHER_PEER"))
-        if (std::atoi(e) != 0 && c->spec) QG_CHECK(qg_comm_set_gather_transport(c, QG_GATHER_PEER));
+        if (std::atoi(e) != 0 && c->spec) {
+            const int st = qg_comm_set_gather_transport(c, QG_GATHER_PEER);
+            if (st == QG_ERR_UNSUPPORTED)
+                std::fprintf(stderr, "qg_mi355: rank %d: QG_GATHER_PEER: peer regions unavailable, the gather stays on RCCL\n", rank);
+            else
+                QG_CHECK(st);
+        }
     return QG_OK;
 }
 

@@ -61,6 +61,10 @@ struct Comm {
     int64_t pg_count = 0;
     int64_t gseq = 0;  // peer record gathers posted
     int64_t *perr_h = nullptr, *perr_d = nullptr;  // a wait timed out: the exchange number
+    // the collective set-up steps' own stream and scratch (allocated at comm_init, so that no
+    // rank can fail before joining region_create's / comm_barrier's all-gathers)
+    hipStream_t coll_s = nullptr;
+    double *coll = nullptr;  // coll_words(nranks) doubles
     uint64_t clock_khz = 100000;
 };
 
@@ -101,6 +105,10 @@ static int comm_setup_watchdog(Comm *c) {
 }
 
 static int post(Comm *c, double *const xbuf[4], int64_t cnt, hipStream_t s);
+
+// region_create: [own handle + status: 16 | all: 16 G | own open status: 8 | all: 8 G];
+// comm_barrier: [1 | G] after those
+static size_t coll_words(int G) { return (size_t)24 * (G + 1) + 1 + (size_t)G; }
 
 // RCCL connects peers lazily, inside the host call of the first operation that needs them
 // (ncclGroupEnd / ncclAllGather), in a handshake with the peer.  A peer that died before its
@@ -149,12 +157,17 @@ int comm_init(void **comm, int nranks, int rank, const char id[128]) {
             return QG_ERR_RCCL;
         }
     }
-    const int w = comm_warmup(c);
+    int w = comm_warmup(c);
+    if (w == QG_OK && (hipStreamCreateWithFlags(&c->coll_s, hipStreamNonBlocking) != hipSuccess ||
+                       hipMalloc((void **)&c->coll, sizeof(double) * coll_words(nranks)) != hipSuccess))
+        w = QG_ERR_HIP;
     if (w != QG_OK) {
         std::fprintf(stderr, "qg_mi355 rank %d/%d: RCCL connection warm-up failed\n", rank, nranks);
         if (c->nccl) ncclCommAbort(c->nccl);
         c->nccl = nullptr;
         if (c->progress_h) (void)hipHostFree(c->progress_h);
+        if (c->coll) (void)hipFree(c->coll);
+        if (c->coll_s) (void)hipStreamDestroy(c->coll_s);
         delete c;
         return w;
     }
@@ -204,6 +217,8 @@ int comm_destroy(void *comm) {
     if (c->nccl) ncclCommDestroy(c->nccl);
     if (c->stage) (void)hipFree(c->stage);
     if (c->progress_h) (void)hipHostFree(c->progress_h);
+    if (c->coll) (void)hipFree(c->coll);
+    if (c->coll_s) (void)hipStreamDestroy(c->coll_s);
     delete c;
     return QG_OK;
 }
@@ -491,65 +506,73 @@ static double *peer_region(double *base, int64_t ld, int par, int dir) {
     return base + PEER_HDR + (size_t)(2 * par + dir) * PEER_ROWS * ld;
 }
 
-// all ranks have reached this point (a one-word all-gather, waited on with the watchdog)
+// all ranks have reached this point (a one-word all-gather, waited on with the watchdog).  The
+// stream and buffer exist since comm_init: no rank returns before the collective.
 static int comm_barrier(Comm *c, const char *what) {
-    double *b = nullptr;
-    hipStream_t s = nullptr;
-    QG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    int st = hipMalloc((void **)&b, sizeof(double) * (size_t)(1 + c->nranks)) == hipSuccess ? QG_OK : QG_ERR_ALLOC;
-    if (st == QG_OK && hipMemsetAsync(b, 0, sizeof(double), s) != hipSuccess) st = QG_ERR_HIP;
-    if (st == QG_OK && ncclAllGather(b, b + 1, 1, ncclDouble, c->nccl, s) != ncclSuccess) st = QG_ERR_RCCL;
-    if (st == QG_OK) st = comm_wait(c, s, nullptr, what);
-    if (b) (void)hipFree(b);
-    (void)hipStreamDestroy(s);
-    return st;
+    double *b = c->coll + 24 * (size_t)(c->nranks + 1);
+    if (hipMemsetAsync(b, 0, sizeof(double), c->coll_s) != hipSuccess) return QG_ERR_HIP;  // (local: before any rank's gather)
+    if (ncclAllGather(b, b + 1, 1, ncclDouble, c->nccl, c->coll_s) != ncclSuccess) return QG_ERR_RCCL;
+    return comm_wait(c, c->coll_s, nullptr, what);
 }
 
 // Collective: allocate this rank's region (`bytes`, uncached, zeroed), all-gather the IPC
 // handles over RCCL and open the regions of the ranks flagged in `need`.  Every rank ends
 // with the same verdict: a rank whose set-up failed makes all of them return
-// QG_ERR_UNSUPPORTED (regions released).
+// QG_ERR_UNSUPPORTED (regions released).  Every rank joins both all-gathers whatever failed
+// locally (the stream and the scratch were made at comm_init): local failures travel in the
+// gathered status words, so no rank waits in a collective another rank skipped.
+//   gather 1: each rank's handle and its set-up status; a rank opens peers' handles only when
+//             every status is OK (never a handle a failed rank did not fill in);
+//   gather 2: each rank's open status.
 static int region_create(Comm *c, Comm::IpcRegion &g, size_t bytes, const std::vector<char> &need, const char *what) {
     const int G = c->nranks;
-    hipStream_t s = nullptr;
-    QG_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    double *hb = nullptr;  // [own handle | all handles | own status | all statuses], 8 words each
-    int st = QG_OK, local = QG_OK;
-    std::vector<hipIpcMemHandle_t> all((size_t)G);
+    hipStream_t s = c->coll_s;
+    double *hb = c->coll;
+    double *own1 = hb, *all1 = hb + 16, *own2 = hb + 16 * (size_t)(G + 1), *all2 = own2 + 8;
+    int local = QG_OK;
     static_assert(sizeof(hipIpcMemHandle_t) == 64, "IPC handle size");
     g.remote.assign((size_t)G, nullptr);
     g.opened.assign((size_t)G, 0);
-    if (hipMalloc((void **)&hb, sizeof(double) * 8 * (size_t)(2 * G + 2)) != hipSuccess) st = QG_ERR_ALLOC;
-    if (st == QG_OK) {
-        if (hipExtMallocWithFlags((void **)&g.local, bytes, hipDeviceMallocUncached) != hipSuccess) g.local = nullptr;
-        if (!g.local || hipMemset(g.local, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+    if (hipExtMallocWithFlags((void **)&g.local, bytes, hipDeviceMallocUncached) != hipSuccess) g.local = nullptr;
+    if (!g.local || hipMemset(g.local, 0, bytes) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+        local = QG_ERR_ALLOC;
+    if (local == QG_OK && !c->perr_h) {
+        if (hipHostMalloc((void **)&c->perr_h, sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&c->perr_d, c->perr_h, 0) != hipSuccess)
             local = QG_ERR_ALLOC;
-        if (local == QG_OK && !c->perr_h) {
-            if (hipHostMalloc((void **)&c->perr_h, sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent) !=
-                    hipSuccess ||
-                hipHostGetDevicePointer((void **)&c->perr_d, c->perr_h, 0) != hipSuccess)
-                local = QG_ERR_ALLOC;
-            else
-                *c->perr_h = 0;
-        }
-        int dev = 0, khz = 0;
-        if (hipGetDevice(&dev) == hipSuccess &&
-            hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
-            c->clock_khz = (uint64_t)khz;
-        hipIpcMemHandle_t h{};
-        if (local == QG_OK && hipIpcGetMemHandle(&h, g.local) != hipSuccess) local = QG_ERR_UNSUPPORTED;
-        if (hipMemcpy(hb, &h, 64, hipMemcpyHostToDevice) != hipSuccess) st = QG_ERR_HIP;
+        else
+            *c->perr_h = 0;
     }
-    if (st == QG_OK && ncclAllGather(hb, hb + 8, 8, ncclDouble, c->nccl, s) != ncclSuccess) st = QG_ERR_RCCL;
+    int dev = 0, khz = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess &&
+        khz > 0)
+        c->clock_khz = (uint64_t)khz;
+    double w1[16] = {};
+    if (local == QG_OK && hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t *>(w1), g.local) != hipSuccess)
+        local = QG_ERR_UNSUPPORTED;
+    w1[8] = (double)local;
+    // (a failed upload leaves the status word unknown to the peers: the gather still runs, and
+    // this rank reports the failure in gather 2)
+    const bool up1 = hipMemcpy(own1, w1, sizeof(w1), hipMemcpyHostToDevice) == hipSuccess;
+    int st = ncclAllGather(own1, all1, 16, ncclDouble, c->nccl, s) == ncclSuccess ? QG_OK : QG_ERR_RCCL;
     if (st == QG_OK) st = comm_wait(c, s, nullptr, what);
-    if (st == QG_OK && hipMemcpy(all.data(), hb + 8, 64 * (size_t)G, hipMemcpyDeviceToHost) != hipSuccess)
-        st = QG_ERR_HIP;
-    for (int r = 0; st == QG_OK && local == QG_OK && r < G; ++r) {
+    if (st != QG_OK) {  // the communicator itself failed (the watchdog aborted it): no gather 2
+        region_release(g);
+        return st;
+    }
+    if (!up1 && local == QG_OK) local = QG_ERR_HIP;
+    std::vector<double> a1(16 * (size_t)G);
+    if (local == QG_OK && hipMemcpy(a1.data(), all1, sizeof(double) * a1.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        local = QG_ERR_HIP;
+    bool all_ok = local == QG_OK;
+    for (int r = 0; all_ok && r < G; ++r) all_ok = a1[16 * (size_t)r + 8] == 0.0;
+    for (int r = 0; all_ok && local == QG_OK && r < G; ++r) {
         if (r == c->rank) {
             g.remote[(size_t)r] = g.local;
         } else if (need[(size_t)r]) {
-            if (hipIpcOpenMemHandle((void **)&g.remote[(size_t)r], all[(size_t)r], hipIpcMemLazyEnablePeerAccess) ==
-                hipSuccess)
+            hipIpcMemHandle_t h;
+            std::memcpy(&h, &a1[16 * (size_t)r], sizeof(h));
+            if (hipIpcOpenMemHandle((void **)&g.remote[(size_t)r], h, hipIpcMemLazyEnablePeerAccess) == hipSuccess)
                 g.opened[(size_t)r] = 1;
             else {
                 g.remote[(size_t)r] = nullptr;
@@ -557,29 +580,24 @@ static int region_create(Comm *c, Comm::IpcRegion &g, size_t bytes, const std::v
             }
         }
     }
-    if (st == QG_OK) {  // agree: the transport switches only if every rank's set-up succeeded
-        double v[8] = {(double)local};
-        if (hipMemcpy(hb + 8 * (size_t)(G + 1), v, 64, hipMemcpyHostToDevice) != hipSuccess) st = QG_ERR_HIP;
-        if (st == QG_OK &&
-            ncclAllGather(hb + 8 * (size_t)(G + 1), hb + 8 * (size_t)(G + 2), 8, ncclDouble, c->nccl, s) != ncclSuccess)
-            st = QG_ERR_RCCL;
-        if (st == QG_OK) st = comm_wait(c, s, nullptr, what);
-        std::vector<double> sts(8 * (size_t)G);
-        if (st == QG_OK &&
-            hipMemcpy(sts.data(), hb + 8 * (size_t)(G + 2), sizeof(double) * sts.size(), hipMemcpyDeviceToHost) !=
-                hipSuccess)
-            st = QG_ERR_HIP;
-        for (int r = 0; st == QG_OK && r < G; ++r)
-            if (sts[8 * (size_t)r] != 0.0) {
-                if (r == c->rank || local == QG_OK)
-                    std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: IPC regions unavailable (rank %d: %s)\n", c->rank,
-                                 G, what, r, qg_strerror((int)sts[8 * (size_t)r]));
-                st = QG_ERR_UNSUPPORTED;
-                break;
-            }
-    }
-    if (hb) (void)hipFree(hb);
-    (void)hipStreamDestroy(s);
+    // gather 2: agree -- the transport switches only if every rank's set-up and opens succeeded
+    double w2[8] = {(double)(local != QG_OK ? local : (all_ok ? QG_OK : QG_ERR_UNSUPPORTED))};
+    if (hipMemcpy(own2, w2, sizeof(w2), hipMemcpyHostToDevice) != hipSuccess && local == QG_OK) local = QG_ERR_HIP;
+    st = ncclAllGather(own2, all2, 8, ncclDouble, c->nccl, s) == ncclSuccess ? QG_OK : QG_ERR_RCCL;
+    if (st == QG_OK) st = comm_wait(c, s, nullptr, what);
+    std::vector<double> sts(8 * (size_t)G);
+    if (st == QG_OK && hipMemcpy(sts.data(), all2, sizeof(double) * sts.size(), hipMemcpyDeviceToHost) != hipSuccess)
+        st = QG_ERR_HIP;
+    if (st == QG_OK && local != QG_OK) st = QG_ERR_UNSUPPORTED;
+    for (int r = 0; st == QG_OK && r < G; ++r)
+        if (sts[8 * (size_t)r] != 0.0) {
+            std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: IPC regions unavailable (rank %d: %s)\n", c->rank, G, what, r,
+                         qg_strerror((int)sts[8 * (size_t)r]));
+            st = QG_ERR_UNSUPPORTED;
+        }
+    if (st == QG_ERR_UNSUPPORTED && local != QG_OK)
+        std::fprintf(stderr, "qg_mi355 rank %d/%d: %s: IPC regions unavailable here (%s)\n", c->rank, G, what,
+                     qg_strerror(local));
     if (st != QG_OK) region_release(g);
     return st;
 }

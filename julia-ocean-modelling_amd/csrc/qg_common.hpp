@@ -36,6 +36,8 @@ constexpr int WAVE = 64;
 // when no halo exchange completes within the transport's timeout.  comm == nullptr: a plain
 // hipStreamSynchronize / hipEventSynchronize.
 int comm_wait(void *comm, hipStream_t s, hipEvent_t ev, const char *what);
+// qg_set_form's value for `which` (QG_FORM_*; 0 = the automatic choice)
+int form(int which);
 int comm_set_timeout(void *comm, double seconds);
 
 __host__ __device__ inline size_t fidx(int64_t i, int64_t j, int64_t ld) {

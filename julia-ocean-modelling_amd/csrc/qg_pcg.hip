@@ -453,7 +453,7 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
             a.pinv_out[2] = -proj_out[2] / det;
             a.pinv_out[3] = proj_out[0] / det;
         }
-        if (std::getenv("QG_PCG_NOCERT")) cert_ = false;  // A/B: the alpha iteration below
+        if (form(QG_FORM_PCG_NO_CERTIFICATE)) cert_ = false;  // (the alpha iteration below)
     }
     rtol_ = rtol > 0 ? rtol : 1e-13;
     maxit_ = maxit > 0 ? maxit : 500;
@@ -491,7 +491,6 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
     gathered_ = a.scal + 64;
     latch_ = gathered_ + 6 * (size_t)nranks;
     cert_part_ = latch_ + 8;
-    if (const char *e = std::getenv("QG_PCG_SYNC")) deferred_ = std::atoi(e) == 0;
     return QG_OK;
 }
 
@@ -690,8 +689,11 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
     // STALL_ITS iterations.  (Unpreconditioned CG decreases by only 1 - 2/sqrt(cond) per
     // iteration -- ~0.98 at 256^2 -- so a short window would stop it on its normal slope: the
     // rule before, "less than 2x over 3 iterations", stopped plain CG at 256^2 at relres 1e-10,
-    // psi 8.8e-9 from the oracle, whatever the target.)
-    constexpr int STALL_ITS = 100;
+    // psi 8.8e-9 from the oracle, whatever the target.)  A preconditioned run converges by
+    // orders of magnitude per iteration until its floor, so its window stays short: a long one
+    // would add up to that many useless iterations to every solve whose target is below the
+    // floor.
+    const int STALL_ITS = precond_ == QG_PRECOND_NONE ? 100 : 3;
     double ref_res = 1e300;
     int ref_it = resume ? 2 : first_it;
     for (int it = resume ? 2 : first_it; it <= maxit_; ++it) {
@@ -714,11 +716,6 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         QG_HIP(hipMemcpyAsync(host, a.scal, sizeof(host), hipMemcpyDeviceToHost, s));
         QG_CHECK(comm_wait(user, s, nullptr, "PCG residual read"));
         iters_ = it;
-        static const bool trace = std::getenv("QG_PCG_TRACE") != nullptr;
-        if (trace)
-            std::fprintf(stderr, "pcg it %d bb %.3e %.3e rr %.3e %.3e alpha %.3e %.3e rz %.3e %.3e\n", it, host[PCG_BB],
-                         host[PCG_BB + 1], host[PCG_RR], host[PCG_RR + 1], host[PCG_ALPHA], host[PCG_ALPHA + 1],
-                         host[PCG_RZ], host[PCG_RZ + 1]);
         bool done = true;
         for (int k = 0; k < 2; ++k) {
             const double bb = host[PCG_BB + k], rr = host[PCG_RR + k];

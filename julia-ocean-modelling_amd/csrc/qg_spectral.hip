@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "qg_fft.hpp"
+#include "qg_fft_lx.hpp"
 #include "qg_spectral.hpp"
 
 namespace qg {
@@ -76,21 +77,29 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     using Plan = FftPlan<N, T>;
     using FwdReg = FftFromReg<N, T, false>;
     using FwdLds = FftFromLds<N, T, false, false>;
+    // N = 4096: the lane-exchange transform (qg_fft_lx.hpp), whose output leaves each thread
+    // the elements g + 512 r of its mirror group g, so the split pairs (k, N - k) meet in
+    // registers; this thread's lines are then k = g + q T
+    constexpr bool LX = N == lx::N && T == lx::T;
     constexpr bool RES_B1 = Plan::REG_IN ? FwdReg::result_in_b1 : FwdLds::result_in_b1;
-    constexpr bool B0_LATE = Plan::REG_IN ? FwdReg::b0_read_late : FwdLds::b0_read_late;
+    constexpr bool B0_LATE = !LX && (Plan::REG_IN ? FwdReg::b0_read_late : FwdLds::b0_read_late);
     extern __shared__ double2 lds[];
-    double2 *b0 = lds, *b1 = Plan::PINGPONG ? lds + LdsSize<N>::value : lds,
-            *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
+    double2 *b0 = lds, *b1 = LX ? lds + N : (Plan::PINGPONG ? lds + LdsSize<N>::value : lds),
+            *twl = LX ? lds + 2 * N : lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
+    double2 *stash = lds + 2 * N + 512;  // (LX: tw512 = twl, then the mirror stash)
     const double2 *Zb = RES_B1 ? b1 : b0;
     // set-up loads first (twiddles, r of the real line k = N/2 (see spec_passB), the first
     // row), their LDS writes after: one memory latency in front of the first row, not one per
     // load
     TwFill<N, T> twf;
-    fft_twiddle_load<N, T>(twf, a.tw);
+    if constexpr (!LX) fft_twiddle_load<N, T>(twf, a.tw);
+    double2 tw5 = make_double2(0, 0);
+    if constexpr (LX) tw5 = a.tw[threadIdx.x];  // W^m, m < 512 (T = 512)
     __shared__ double crN[2];
     double crv = 0;
     if (threadIdx.x < 2) crv = QG_CR(threadIdx.x * a.KS + NH);
     const int t = threadIdx.x, c = blockIdx.x;
+    const int g = LX ? lx::mirror_group(t) : t;  // lines k = g + q T
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
     const int64_t ld = a.ld;
@@ -138,7 +147,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const int k = t + q * T;
+                const int k = g + q * T;
                 rqh[q][s] = (NH % T == 0 || k < NH) ? QG_CR(s * KS + k) : 0.0;
             }
     }
@@ -155,12 +164,21 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const int k = t + q * T;
+                const int k = g + q * T;
                 if constexpr (COEF_HOIST) rq[q][s] = rqh[q][s];
                 else if (NH % T == 0 || k < NH) rq[q][s] = QG_CR(s * KS + k);
             }
 #define QG_PA_R(q, s, o) rq[q][s]
-        if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
+        double2 zr[8];  // LX: Z_(g + 512 r) after the transform and the mirror exchange
+        if constexpr (LX) {
+#pragma unroll
+            for (int p = 0; p < EP; ++p) zr[p] = make_double2(p0 * c1[p] + p1 * c2[p], p2 * c1[p] + p3 * c2[p]);
+            const int tt = opaque_tid();
+            lx::fft<false, false, true>(zr, b0, b1, twl, tt, [&]() {
+                if (PF && j - 1 >= s0) load_into(j - 1, c1, c2);
+            });
+            lx::mirror_exchange(zr, stash, tt);
+        } else if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
             double2 in[Plan::R0];
 #pragma unroll
             for (int p = 0; p < EP; ++p) in[p] = make_double2(p0 * c1[p] + p1 * c2[p], p2 * c1[p] + p3 * c2[p]);
@@ -180,11 +198,21 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
-            const int k = t + q * T;
+            const int k = g + q * T;
             if (NH % T == 0 || k < NH) {
-                const double2 Zk = Zb[lay<Plan::LAST_NS>(k)];
+                // Z_k and its split partner Z_(N-k) (k = 0: Z_(N/2)).  LX: register q and the
+                // partner lane's register 7 - q, now in register 7 - q (thread 0, group 0, is
+                // its own partner: Z_(512 (8 - q)), Z_2048 in register 4)
+                double2 Zk, Zm;
+                if constexpr (LX) {
+                    Zk = zr[q];
+                    Zm = t == 0 ? zr[q == 0 ? 4 : (8 - q) & 7] : zr[7 - q];
+                } else {
+                    Zk = Zb[lay<Plan::LAST_NS>(k)];
+                    Zm = Zb[lay<Plan::LAST_NS>(k == 0 ? NH : N - k)];
+                }
                 if (k == 0) {  // the two real lines k = 0 and k = N/2
-                    const double2 Zn = Zb[lay<Plan::LAST_NS>(NH)];
+                    const double2 Zn = Zm;
                     dc += Zk.x;
                     hline[j] = Zk.x;
                     const double2 B[2] = {make_double2(Zk.x, Zn.x), make_double2(Zk.y, Zn.y)};
@@ -195,13 +223,16 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                         (void)o0;
                         u[q][s] = make_double2((r0 * a.csc) * B[s].x + r0 * u[q][s].x,
                                                (rN * a.csc) * B[s].y + rN * u[q][s].y);
-                        st_u(Urow + s * KS, Store<S>::c(make_double2(u[q][s].x, 0)));
-                        st_u(Urow + s * KS + NH, Store<S>::c(make_double2(u[q][s].y, 0)));
+                        if constexpr (LX) {  // slot order: the pair packed in slot 0
+                            st_u(Urow + s * KS, Store<S>::c(u[q][s]));
+                        } else {
+                            st_u(Urow + s * KS, Store<S>::c(make_double2(u[q][s].x, 0)));
+                            st_u(Urow + s * KS + NH, Store<S>::c(make_double2(u[q][s].y, 0)));
+                        }
                         bw[q][s] = make_double2(om[q][s].x * u[q][s].x + bw[q][s].x, om[q][s].y * u[q][s].y + bw[q][s].y);
                         om[q][s] = make_double2(om[q][s].x * r0, om[q][s].y * rN);
                     }
                 } else {
-                    const double2 Zm = Zb[lay<Plan::LAST_NS>(N - k)];
                     const double2 B[2] = {make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5),
                                           make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5)};
 #pragma unroll
@@ -210,7 +241,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                         const double r = QG_PA_R(q, s, o);  // cs = r csc
                         (void)o;
                         u[q][s] = cfma(r, u[q][s], cscale(B[s], r * a.csc));
-                        st_u(Urow + s * KS + k, Store<S>::c(u[q][s]));
+                        st_u(Urow + s * KS + (LX ? t + q * T : k), Store<S>::c(u[q][s]));
                         bw[q][s] = cfma(om[q][s].x, u[q][s], bw[q][s]);
                         om[q][s].x *= r;
                     }
@@ -221,13 +252,14 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
     };
 #undef QG_PA_R
     if constexpr (PF) load_into(e, pf1, pf2);
-    fft_twiddle_store<N, T>(twl, twf);
+    if constexpr (LX) twl[t] = tw5;
+    else fft_twiddle_store<N, T>(twl, twf);
     if (threadIdx.x < 2) crN[threadIdx.x] = crv;
     __syncthreads();
     for (int j = e; j >= s0; --j) row_step(j, pf1, pf2);
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
-        const int k = t + q * T;
+        const int k = g + q * T;
         if (NH % T == 0 || k < NH) {
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
@@ -685,16 +717,25 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     constexpr int T = G::T, KQ = G::KQ, EP = G::EP, NH = N / 2;
     using Plan = FftPlan<N, T>;
     using Inv = FftFromLds<N, T, true, Plan::REG_OUT>;
+    // N = 4096: the lane-exchange transform (see spec_passA): a thread's lines are k = g + q T
+    // of its mirror group g; it forms Z_k and Z_(N-k) in registers q and 7 - q, the mirror
+    // exchange gives every thread its whole group, and the inverse transform leaves the row in
+    // the coalesced order of the stores (no LDS write of the spectrum)
+    constexpr bool LX = N == lx::N && T == lx::T;
     extern __shared__ double2 lds[];
-    double2 *b0 = lds, *b1 = Plan::PINGPONG ? lds + LdsSize<N>::value : lds,
-            *twl = lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
+    double2 *b0 = lds, *b1 = LX ? lds + N : (Plan::PINGPONG ? lds + LdsSize<N>::value : lds),
+            *twl = LX ? lds + 2 * N : lds + (Plan::PINGPONG ? 2 : 1) * LdsSize<N>::value;
+    double2 *stash = lds + 2 * N + 512;  // (LX: tw512 = twl, then the mirror stash)
     const double2 *Xb = Inv::result_in_b1 ? b1 : b0;
     // set-up loads (twiddles, the chunk's singular-line values, (r, 1/r) of k = N/2) go out
     // first and reach LDS just before pin_total's barrier (a serial head would put
     // one memory latency per load in front of the first row's loads)
     TwFill<N, T> twf;
-    fft_twiddle_load<N, T>(twf, a.tw);
+    if constexpr (!LX) fft_twiddle_load<N, T>(twf, a.tw);
+    double2 tw5 = make_double2(0, 0);
+    if constexpr (LX) tw5 = a.tw[threadIdx.x];  // W^m, m < 512 (T = 512)
     const int t = threadIdx.x, c = blockIdx.x;
+    const int g = LX ? lx::mirror_group(t) : t;  // lines k = g + q T
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     // the chunk's values of the singular line, staged once (a global load per row would sit
     // on every row's critical path, in front of the transform's barriers)
@@ -725,11 +766,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS;
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
-            const int k = t + q * T;
+            const int k = g + q * T;
             if (NH % T == 0 || k < NH) {
 #pragma unroll
                 for (int s = 0; s < 2; ++s) {
-                    if (k == 0) {
+                    if constexpr (LX) {
+                        upf[q][s] = Urow[s * KS + t + q * T];  // slot order (see spec_passA)
+                    } else if (k == 0) {
                         upf[q][s].x = Urow[s * KS].x;
                         upf[q][s].y = Urow[s * KS + NH].x;
                     } else {
@@ -746,7 +789,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     double2 cu[KQ][2], w[KQ][2];
 #pragma unroll
     for (int q = 0; q < KQ; ++q) {
-        const int k = t + q * T;
+        const int k = g + q * T;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             cu[q][s] = make_double2(0, 0);
@@ -772,8 +815,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         for (int q = 0; q < KQ; ++q)
 #pragma unroll
             for (int s = 0; s < 2; ++s) {
-                const int k = t + q * T;
-                if (NH % T == 0 || k < NH) crq[q][s] = QG_CRR(s * KS + k);
+                const int k = g + q * T;
+                if (NH % T == 0 || k < NH) crq[q][s] = LX ? a.scrr[s * KS + t + q * T] : QG_CRR(s * KS + k);
             }
     };
     load_coef();
@@ -781,7 +824,8 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
     // folded after the chunk set-up, so the carries' loads are not queued behind the pin
     // parts' (folding first: 4096^2 pass B 125.9 -> 137.9 us); its barrier also publishes
     // lline and the twiddles
-    fft_twiddle_store<N, T>(twl, twf);
+    if constexpr (LX) twl[t] = tw5;
+    else fft_twiddle_store<N, T>(twl, twf);
     if (a.pinned0 && t < L) lline[t] = llv;
     if (N < 4096 && t < 2) crN[t] = crv;
     const double pin = pin_total<T>(pinp, pinw);
@@ -797,9 +841,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         // compiler memory barrier: re-read the (L1-resident) coefficients every row instead of
         // hoisting them into registers, which would spill at this occupancy
         asm volatile("" ::: "memory");
+        // LX: Z_k in register q, Z_(N-k) in register 7 - q (the partner lane's after the
+        // exchange); thread 0 (group 0, its own partner) keeps Z_(512 (8 - q)) in register 8 - q
+        // and Z_2048 in register 4
+        double2 zr[8], zm[KQ];
 #pragma unroll
         for (int q = 0; q < KQ; ++q) {
-            const int k = t + q * T;
+            const int k = g + q * T;
             if (NH % T == 0 || k < NH) {
                 double2 X[2];
                 if (k == 0) {
@@ -821,8 +869,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                         x0[s] = (s == 0 && sing) ? (line0 + (double)j * line1) + lline[j - s0] : wx;
                         xN[s] = wy;
                     }
-                    b0[0] = make_double2(x0[0], x0[1]);
-                    b0[NH] = make_double2(xN[0], xN[1]);
+                    if constexpr (LX) {
+                        zr[q] = make_double2(x0[0], x0[1]);
+                        zm[q] = make_double2(xN[0], xN[1]);
+                    } else {
+                        b0[0] = make_double2(x0[0], x0[1]);
+                        b0[NH] = make_double2(xN[0], xN[1]);
+                    }
                 } else {
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
@@ -834,14 +887,35 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
                         cu[q][s] = cscale(cu[q][s], rr.y);
                         X[s] = w[q][s];
                     }
-                    b0[k] = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
-                    b0[N - k] = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
+                    const double2 zk = make_double2(X[0].x - X[1].y, X[0].y + X[1].x);
+                    const double2 zn = make_double2(X[0].x + X[1].y, X[1].x - X[0].y);
+                    if constexpr (LX) {
+                        zr[q] = zk;
+                        zm[q] = zn;
+                    } else {
+                        b0[k] = zk;
+                        b0[N - k] = zn;
+                    }
                 }
             }
         }
-        __syncthreads();
         double2 xo[Plan::R_LAST];  // last FFT pass output in registers: element t + r*T
-        Inv::run(b0, b1, twl, xo);
+        if constexpr (LX) {
+            static_assert(KQ == 4 && Plan::R_LAST == 8, "lane-exchange geometry");
+            const bool t0 = t == 0;
+            zr[4] = t0 ? zm[0] : zm[3];
+            zr[5] = t0 ? zm[3] : zm[2];
+            zr[6] = t0 ? zm[2] : zm[1];
+            zr[7] = t0 ? zm[1] : zm[0];
+            const int tt = opaque_tid();
+            lx::mirror_exchange(zr, stash, tt);
+            lx::fft<true, true, false>(zr, b0, b1, twl, tt);
+#pragma unroll
+            for (int p = 0; p < 8; ++p) xo[p] = zr[p];
+        } else {
+            __syncthreads();
+            Inv::run(b0, b1, twl, xo);
+        }
         S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
         S *row1 = out1 + (size_t)(j + 1) * ld;
         const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
@@ -864,7 +938,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
         }
         asm volatile("" ::: "memory");
         if (j < e) load_coef();
-        if constexpr (Inv::b0_read_late) __syncthreads();  // the next row's recurrence writes b0
+        if constexpr (!LX && Inv::b0_read_late) __syncthreads();  // the next row's recurrence writes b0
     }
 #undef QG_PB_R
 }
@@ -873,8 +947,13 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 // Wide rows (M = 8192).  Both systems' recurrence state (4 complex per wavenumber) plus a
 // 8192-point transform do not fit in one CU's registers and LDS, so each workgroup serves ONE
 // system of a chunk: its real row x (length M) is transformed as the half-length complex
-// FFT of z_n = x_2n + i x_2n+1 (the tuned 4096-point, 512-thread plan: ping-pong LDS buffers,
-// register-fed first pass) plus a split step X_k = E_k + W^k O_k, W = exp(-2 pi i / M).
+// FFT of z_n = x_2n + i x_2n+1 (the 4096-point, 512-thread lane-exchange transform,
+// qg_fft_lx.hpp) plus a split step X_k = E_k + W^k O_k, W = exp(-2 pi i / M).  The transform
+// leaves a thread the elements g + 512 r of its mirror group g and, after the mirror exchange,
+// the partner group's registers 4-7, so a thread's lines are
+//   k_q = g + 512 q (q < 4),  k_q = (512 - g) + 512 q (q >= 4)     (thread 0: k_q = 512 q)
+// and the split partner HN - k_q of line q is the thread's own line 7 - q: the split step of
+// both passes runs in registers (no LDS round trip for the pairs).
 // Pass A: one launch, workgroups (chunk, system) adjacent in XCD-aware order so the two
 // readers of a row of zeta share an L2 and run side by side.  Pass B: two launches; system 0 leaves psi~1 rows in half_tmp
 // (F64), system 1 combines them with psi~2 into the back-projection and the ghost ring.
@@ -882,31 +961,29 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passB(SpecArgs a
 // ------------------------------------------------------------------------------------
 constexpr int HN = 4096;           // half-length FFT
 constexpr int HT = 512;            // threads per workgroup
-constexpr int HK = HN / HT;        // wavenumber slots per thread: k = t + q*HT; slot (q 0, t 0)
+constexpr int HK = HN / HT;        // wavenumber slots per thread (k_q above); slot (q 0, t 0)
                                    // packs the real lines k = 0 (.x) and k = HN (.y)
-using HPlan = FftPlan<HN, HT>;
-static_assert(HPlan::REG_IN && HPlan::PINGPONG && HPlan::R0 == HK, "wide-row plan");
-// LDS: the two row buffers and the pass twiddles, then the two-level split-step twiddles
-// (64 + 64).  (The transforms stay F64 for F32 states too: computing pass A's in F32 saved
+static_assert(HN == lx::N && HT == lx::T && HK == 8, "wide-row transform geometry");
+// LDS: the transform's two row buffers, its twiddles and the mirror stash (lx::LDS_ELEMS),
+// then the two-level split-step twiddles (64 + 64).  (The transforms stay F64 for F32 states too: computing pass A's in F32 saved
 // 18 of 392 us at 8192^2 and pass B's 16 of 417, while the F32 error grew -- psi 2.3e-3 ->
 // 5.3e-3 against the oracle at 8192 x 16, zeta 1e-4 -> 1e-3 on the smooth field with pass B's
 // in F32 (r04e; qg_fft.hpp keeps the complex type a template parameter).)
-template <class CX>
-constexpr size_t half_lds_bytes() {
-    return sizeof(CX) * (2 * LdsSize<HN>::value + HPlan::TW) + sizeof(double2) * 128;
-}
-template <class CX>
+constexpr size_t half_lds_bytes() { return sizeof(double2) * (lx::LDS_ELEMS + 128); }
 struct HalfLds {
-    CX *b0, *b1, *twl;
-    double2 *wlo, *whi;
+    double2 *b0, *b1, *tw512, *stash, *wlo, *whi;
     __device__ explicit HalfLds(void *base) {
-        b0 = static_cast<CX *>(base);
-        b1 = b0 + LdsSize<HN>::value;
-        twl = b1 + LdsSize<HN>::value;
-        wlo = reinterpret_cast<double2 *>(twl + HPlan::TW);
+        b0 = static_cast<double2 *>(base);
+        b1 = b0 + HN;
+        tw512 = b1 + HN;
+        stash = tw512 + 512;
+        wlo = b0 + lx::LDS_ELEMS;
         whi = wlo + 64;
     }
 };
+// line q of thread t (mirror group g, partner group gm = 512 - g; groups 0 and 256 are their
+// own partners)
+__device__ __forceinline__ int half_line(int g, int gm, int q) { return (q < HK / 2 ? g : gm) + q * HT; }
 
 template <class S>
 struct Pair;  // two adjacent row elements (8-byte / 4-byte alignment: rows start at element 1)
@@ -923,18 +1000,16 @@ __device__ __forceinline__ double2 half_tw(const double2 *wlo, const double2 *wh
     return cmul(wlo[k & 63], whi[k >> 6]);
 }
 
-template <class C>
-__device__ __forceinline__ void half_lds_init(const SpecArgs &a, C *twl, double2 *wlo, double2 *whi) {
+__device__ __forceinline__ void half_lds_init(const SpecArgs &a, double2 *tw512, double2 *wlo, double2 *whi) {
     // every load in flight before the first LDS write (one memory latency, not one per table)
-    TwFill<HN, HT> twf;
-    fft_twiddle_load<HN, HT>(twf, a.tw2);
     const int t = threadIdx.x;
+    const double2 tw5 = a.tw2[t];  // W_4096^m, m < 512 (HT = 512)
     double2 lo = make_double2(0, 0), hi = make_double2(0, 0);
     if (t < 64) {
         lo = a.tw[t];
         hi = a.tw[64 * t];
     }
-    fft_twiddle_store<HN, HT>(twl, twf);
+    tw512[t] = tw5;
     if (t < 64) {
         wlo[t] = lo;
         whi[t] = hi;
@@ -946,18 +1021,17 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     using US = typename Store<S>::C;
     using PV = typename Pair<S>::V;
     using CX = double2;
-    using Fwd = FftFromReg<HN, HT, false, CX>;
     extern __shared__ double2 lds[];
-    const HalfLds<CX> hl(lds);
-    CX *b0 = hl.b0, *b1 = hl.b1, *twl = hl.twl;
+    const HalfLds hl(lds);
+    double2 *b0 = hl.b0, *b1 = hl.b1, *tw512 = hl.tw512, *stash = hl.stash;
     double2 *wlo = hl.wlo, *whi = hl.whi;
-    const CX *Zb = Fwd::result_in_b1 ? b1 : b0;
-    half_lds_init(a, twl, wlo, whi);
+    half_lds_init(a, tw512, wlo, whi);
     __syncthreads();
     // the two workgroups of a chunk read the same input rows: XCD-aware order puts them on
     // one XCD (one L2) side by side
     const int wg = xcd_logical_id();
     const int t = threadIdx.x, c = wg >> 1, s = wg & 1;
+    const int g = lx::mirror_group(t), gm = g == 0 ? 0 : 512 - g;
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
     const int64_t ld = a.ld;
@@ -981,7 +1055,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
             d2[p] = *reinterpret_cast<const PV *>(r2 + 2 * n);
         }
     };
-    const double *cr = a.cr + s * KS;
+    const double *cr = a.cr + s * KS, *scr = a.scr + s * KS;
     const double csc = a.csc;
     // one row: consume the prefetched row (c1, c2), refill them with row jn (< s0: none)
     auto row_step = [&](int j, PV(&c1)[HK], PV(&c2)[HK], int jn) {
@@ -991,20 +1065,19 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         for (int p = 0; p < HK; ++p)
             in[p] = make_double2(pa * (double)c1[p].x + pb * (double)c2[p].x,
                                  pa * (double)c1[p].y + pb * (double)c2[p].y);
-        // first pass from registers, then the next row's loads (in[] is dead by then: fewer
-        // live registers than loading first), then the remaining passes
+        // the transform (the next row's loads issued once the first stage has left in[] in
+        // LDS: fewer live registers than loading first) and the mirror exchange: in[q] =
+        // Z_(k_q), in[7 - q] = Z_(HN - k_q)
         const int tt = opaque_tid();
-        fft_pass<HN, HT, 1, 0, false, true, false>((const CX *)nullptr, b0, twl, tt, in);
-        if (jn >= s0) load_row(jn, c1, c2);
-        {
-            CX dummy[HPlan::R_LAST];
-            fft_run<HN, HT, HPlan::R0, 1, false, false>(b0, b1, twl, tt, dummy);
-        }
+        lx::fft<false, false, true>(in, b0, b1, tw512, tt, [&]() {
+            if (jn >= s0) load_row(jn, c1, c2);
+        });
+        lx::mirror_exchange(in, stash, tt);
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
-            const int k = t + q * HT;
-            const double2 Zk = Zb[lay<HPlan::LAST_NS>(k)];
+            const int k = half_line(g, gm, q);
+            const double2 Zk = in[q];
             if (k == 0) {  // X_0 = Re + Im, X_HN = Re - Im of Z_0 (both real)
                 const double X0 = Zk.x + Zk.y, XN = Zk.x - Zk.y;
                 if (s == 0) {
@@ -1013,30 +1086,28 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 }
                 const double r0 = cr[0], rN = cr[HN];
                 u[q] = make_double2((r0 * csc) * X0 + r0 * u[q].x, (rN * csc) * XN + rN * u[q].y);
-                st_u(Urow, Store<S>::c(make_double2(u[q].x, 0)));
-                st_u(Urow + HN, Store<S>::c(make_double2(u[q].y, 0)));
+                st_u(Urow, Store<S>::c(u[q]));  // slot order: the pair packed in slot 0
                 bw[q] = make_double2(om[q].x * u[q].x + bw[q].x, om[q].y * u[q].y + bw[q].y);
                 om[q] = make_double2(om[q].x * r0, om[q].y * rN);
             } else {
-                const double2 Zm = Zb[lay<HPlan::LAST_NS>(HN - k)];
+                const double2 Zm = t == 0 ? in[(8 - q) & 7] : in[7 - q];  // Z_(HN - k)
                 // E = (Z_k + conj Z_{HN-k}) / 2, O = (Z_k - conj Z_{HN-k}) / 2i, X = E + W^k O
                 const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                 const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
                 const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
-                const double r = cr[k];
+                const double r = scr[t + q * HT];
                 u[q] = cfma(r, u[q], cscale(X, r * csc));
-                st_u(Urow + k, Store<S>::c(u[q]));
+                st_u(Urow + t + q * HT, Store<S>::c(u[q]));
                 bw[q] = cfma(om[q].x, u[q], bw[q]);
                 om[q].x *= r;
             }
         }
-        if constexpr (Fwd::b0_read_late) __syncthreads();  // the next row's first pass writes b0
     };
     load_row(e, pf1, pf2);
     for (int j = e; j >= s0; --j) row_step(j, pf1, pf2, j - 1);
 #pragma unroll
     for (int q = 0; q < HK; ++q) {
-        const int k = t + q * HT;
+        const int k = half_line(g, gm, q);
         const size_t o = ((size_t)c * 2 + s) * KS;
         if (k == 0) {
             a.ULS[o] = make_double2(u[q].x, 0);
@@ -1061,14 +1132,12 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     constexpr int s = SYS;
     using CX = double2;
     extern __shared__ double2 lds[];
-    const HalfLds<CX> hl(lds);
-    CX *b0 = hl.b0, *b1 = hl.b1, *twl = hl.twl;
+    const HalfLds hl(lds);
+    double2 *b0 = hl.b0, *b1 = hl.b1, *tw512 = hl.tw512, *stash = hl.stash;
     double2 *wlo = hl.wlo, *whi = hl.whi;
-    // the split step exchanges X through b1: the first inverse pass writes only b0
-    CX *Xs = b1;
-    static_assert(HPlan::REG_OUT && HPlan::NPASS == 4, "last pass to registers, reading b0");
-    half_lds_init(a, twl, wlo, whi);
+    half_lds_init(a, tw512, wlo, whi);
     const int t = threadIdx.x, c = blockIdx.x;
+    const int g = lx::mirror_group(t), gm = g == 0 ? 0 : 512 - g;
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     __shared__ double lline[64];  // L <= 64 (pick_chunk)
     __shared__ double pinw[HT / 64];
@@ -1082,22 +1151,14 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     const double delta = a.scal[0];
     const bool inject = a.pinned0 && a.rank == 0;
     const double line0 = a.scal[2], line1 = a.scal[3];
-    const double2 *crr = a.crr + s * KS;
+    const double2 *crr = a.crr + s * KS, *scrr = a.scrr + s * KS;
     const double *ccs = a.ccs + s * KS;
 
     US upf[HK];  // (storage precision until used: see spec_passB)
     auto load_u = [&](int j) {
         const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
 #pragma unroll
-        for (int q = 0; q < HK; ++q) {
-            const int k = t + q * HT;
-            if (k == 0) {
-                upf[q].x = Urow[0].x;
-                upf[q].y = Urow[HN].x;
-            } else {
-                upf[q] = Urow[k];
-            }
-        }
+        for (int q = 0; q < HK; ++q) upf[q] = Urow[t + q * HT];  // slot order (see spec_passA_half)
     };
     load_u(s0);
     // folded before the chunk set-up, whose registers are short here (the pin loads were
@@ -1108,7 +1169,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     double2 cu[HK], w[HK];
 #pragma unroll
     for (int q = 0; q < HK; ++q) {
-        const int k = t + q * HT;
+        const int k = half_line(g, gm, q);
         if (k == 0) {
             double2 c0 = make_double2(0, 0), w0 = make_double2(0, 0), cN, wN;
             if (!sing) chunk_carry(a, s, 0, c, delta, inject, c0, w0);
@@ -1133,7 +1194,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     double2 crq[HK];
     auto load_coef = [&]() {
 #pragma unroll
-        for (int q = 0; q < HK; ++q) crq[q] = crr[t + q * HT];
+        for (int q = 0; q < HK; ++q) crq[q] = scrr[t + q * HT];
     };
     if constexpr (EARLY) load_coef();
     for (int j = s0; j <= e; ++j) {
@@ -1144,7 +1205,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
         double x0 = 0;  // slot (q 0, t 0): X_0 (.x of w, or the singular line)
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
-            const int k = t + q * HT;
+            const int k = half_line(g, gm, q);
             if (k == 0) {
                 double ul0 = ucur[q].x, ulN = ucur[q].y;
                 if (s == 0 && inject && j == 0) {  // Poisson compatibility shift at row 0
@@ -1160,37 +1221,40 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
             } else {
                 double2 ul = ucur[q];
                 if (s == 0 && inject && j == 0) ul.x += ccs[k] * delta;
-                const double2 rr = EARLY ? crq[q] : crr[k];
+                const double2 rr = EARLY ? crq[q] : scrr[t + q * HT];
                 w[q] = cfma(rr.x, w[q], cadd(ul, cu[q]));
                 cu[q] = cscale(cu[q], rr.y);
-                Xs[k] = w[q];
             }
         }
-        __syncthreads();
-        // Z_k = (X_k + conj X_{HN-k}) + i W^-k (X_k - conj X_{HN-k}); z = IDFT(Z) = x_2n + i x_2n+1
+        // Z_k = (X_k + conj X_{HN-k}) + i W^-k (X_k - conj X_{HN-k}); z = IDFT(Z) = x_2n + i x_2n+1.
+        // X_(HN - k_q) is this thread's line 7 - q (thread 0: line (8 - q) mod 8).  Z_(k_q) goes
+        // to register q: for q >= 4 that is the partner group's register, which the mirror
+        // exchange delivers.
         CX in[HK];
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
-            const int k = t + q * HT;
+            const int k = half_line(g, gm, q);
             if (k == 0) {
                 in[q] = make_double2(x0 + w[q].y, x0 - w[q].y);
             } else {  // X_k = w[q]
-                const double2 Xm = Xs[HN - k];
+                const double2 Xm = t == 0 ? w[(8 - q) & 7] : w[7 - q];
                 const double2 A = make_double2(w[q].x + Xm.x, w[q].y - Xm.y);
                 const double2 D = make_double2(w[q].x - Xm.x, w[q].y + Xm.y);
                 const double2 B = cmul(cconj(half_tw(wlo, whi, k)), D);
                 in[q] = make_double2(A.x - B.y, A.y + B.x);
             }
         }
-        // first inverse pass, then the next row's loads (in[] dead), then the remaining passes;
-        // the last pass leaves its output in registers (element t + p HT: the row order of the
-        // stores below), so a row writes the LDS four times (split step + three passes), not five
+        // the mirror exchange, then the transform (the next row's loads once the first stage
+        // has left in[] in LDS); the output is element t + p HT of the row in register p, the
+        // order of the stores below.  A row writes the LDS twice (the transform's two
+        // transposes).
         const int tt = opaque_tid();
-        fft_pass<HN, HT, 1, 0, true, true, false>((const CX *)nullptr, b0, twl, tt, in);
-        if (j < e) load_u(j + 1);
-        if constexpr (SYS == 1) load_y(j);
-        CX xo[HPlan::R_LAST];
-        fft_run<HN, HT, HPlan::R0, 1, true, true>(b0, b1, twl, tt, xo);
+        lx::mirror_exchange(in, stash, tt);
+        lx::fft<true, true, false>(in, b0, b1, tw512, tt, [&]() {
+            if (j < e) load_u(j + 1);
+            if constexpr (SYS == 1) load_y(j);
+        });
+        const CX(&xo)[HK] = in;
         // SYS 0: the next row's (r, 1/r) before this row's stores -- vmcnt counts loads and
         // stores in order, so loaded after them the next recurrence waited for every store of
         // this row (8192^2 F32 B0: 187 -> 179 us; the 4096-point pass B, at its register
@@ -1245,15 +1309,14 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                 }
             }
         }
-        // (no barrier: the last pass read b0, and the next row's first write of b0 follows the
-        // split step's barrier; b1, which the next split step writes, was last read by the
-        // third pass, before its own barrier)
+        // (no barrier: the transform's buffers are safe to reuse by the next row's, see
+        // lx::fft)
     }
 }
 
 template <class S>
 static int launch_half_t(bool passB, const SpecArgs &a, hipStream_t s) {
-    const size_t lds = half_lds_bytes<double2>();
+    const size_t lds = half_lds_bytes();
     if (passB) {
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB_half<S, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -2022,7 +2085,8 @@ __global__ __launch_bounds__(SPL_KT) void spec_passB_split(SpecArgs a) {
 // ------------------------------------------------------------------------------------
 template <int N, class S>
 static int launch_pass_t(bool passB, const SpecArgs &a, hipStream_t s) {
-    const size_t lds = sizeof(double2) * FftPlan<N, Geo<N>::T>::LDS;
+    constexpr bool LX = N == lx::N && Geo<N>::T == lx::T;  // (the lane-exchange transform)
+    const size_t lds = sizeof(double2) * (LX ? (size_t)lx::LDS_ELEMS : (size_t)FftPlan<N, Geo<N>::T>::LDS);
     if (passB) {
         QG_HIP(hipFuncSetAttribute((const void *)spec_passB<N, S>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         spec_passB<N, S><<<a.Nc, Geo<N>::T, lds, s>>>(a);
@@ -2054,8 +2118,8 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
         case 8192: return a.f32 ? launch_half_t<float>(passB, a, s) : launch_half_t<double>(passB, a, s);
         default: break;
     }
-    // (QG_SPLIT_FORCE: tests run generic-size rows through the split passes)
-    if (a.M > GEN_MMAX || std::getenv("QG_SPLIT_FORCE") != nullptr) {
+    // (qg_set_form(QG_FORM_ROW_SPLIT, 1): generic-size rows through the split passes too)
+    if (a.M > GEN_MMAX || form(QG_FORM_ROW_SPLIT)) {
         if (a.M > SPL_WMAX || (a.M > SPL_MMAX && a.M % 2 != 0)) return QG_ERR_UNSUPPORTED;
         const bool wsplit = a.M > SPL_MMAX;  // half-length transforms, one system at a time
         const bool wpow2 = a.M == 2 * SPL_MMAX;  // (the tuned 8192-point plan)
@@ -2218,7 +2282,7 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     // ---- device memory ---------------------------------------------------------------
     const size_t n_tw = align_up(sizeof(double2) * M);
     const size_t n_coef = align_up(sizeof(Coef) * coef.size());
-    const size_t n_hot = align_up(sizeof(double) * 8 * (size_t)KS);
+    const size_t n_hot = align_up(sizeof(double) * 14 * (size_t)KS);
     const size_t n_U = align_up(sizeof(double2) * (size_t)P * 2 * KS);
     const size_t n_S = align_up(sizeof(double2) * (size_t)a.Nc * 2 * KS);
     const size_t n_dc = align_up(sizeof(double) * a.Nc);
@@ -2292,18 +2356,33 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     }
     QG_HIP(hipMemcpy(d_coef, coef.data(), sizeof(Coef) * coef.size(), hipMemcpyHostToDevice));
     {
-        // [2][KS] (r, 1/r) pairs, [2][KS] cs, [2][KS] r
-        std::vector<double> hot(8 * (size_t)KS);
+        // [2][KS] (r, 1/r) pairs, [2][KS] cs, [2][KS] r; slot order: [2][KS] (r, 1/r), [2][KS] r
+        std::vector<double> hot(14 * (size_t)KS);
         for (size_t i = 0; i < 2 * (size_t)KS; ++i) {
             hot[2 * i] = coef[i].r;
             hot[2 * i + 1] = coef[i].rinv;
             hot[4 * KS + i] = coef[i].cs;
             hot[6 * KS + i] = coef[i].r;
         }
+        if (M == lx::N || M == 2 * lx::N) {
+            const int lines = M == lx::N ? 4 : 8;  // per thread and system
+            for (int s = 0; s < 2; ++s)
+                for (int t = 0; t < lx::T; ++t)
+                    for (int q = 0; q < lines; ++q) {
+                        const int g = lx::mirror_group(t), gm = g == 0 ? 0 : 512 - g;
+                        const size_t k = (size_t)((q < 4 ? g : gm) + 512 * q), slot = (size_t)(t + 512 * q);
+                        const Coef &cf = coef[(size_t)s * KS + k];
+                        hot[8 * KS + 2 * (s * KS + slot)] = cf.r;
+                        hot[8 * KS + 2 * (s * KS + slot) + 1] = cf.rinv;
+                        hot[12 * KS + s * KS + slot] = cf.r;
+                    }
+        }
         QG_HIP(hipMemcpy(d_hot, hot.data(), sizeof(double) * hot.size(), hipMemcpyHostToDevice));
         a.crr = reinterpret_cast<const double2 *>(d_hot);
         a.ccs = d_hot + 4 * KS;
         a.cr = d_hot + 6 * KS;
+        a.scrr = reinterpret_cast<const double2 *>(d_hot + 8 * KS);
+        a.scr = d_hot + 12 * KS;
         a.csc = -(dx * dx) / (double)M;
     }
     QG_HIP(hipMemset(a.rec, 0, n_rec));

@@ -54,7 +54,14 @@ struct SpecArgs {
     const double *ccs;        // [2][KS] cs of coef
     const double *cr;         // [2][KS] r of coef: pass A's one 8-byte load per line and row
     double csc;               // -dx^2 / M: cs = r csc (pass A forms cs on the fly)
-    void *U;                  // [P][2][KS] complex (double2, or float2 for F32 states)
+    // M = 4096 / 8192 (the lane-exchange passes): r and (r, 1/r) in SLOT order, [2][KS] with
+    // slot t + 512 q holding thread t's line q (qg_fft_lx.hpp's mirror groups); the passes also
+    // keep u in slot order (U is private to them), so every row access is one aligned run per
+    // wave.  Slot 0 of thread 0 is the line k = 0 (u packs k = 0 and k = M/2 there).
+    const double *scr;
+    const double2 *scrr;
+    void *U;                  // [P][2][KS] complex (double2, or float2 for F32 states); k order,
+                              // slot order in the lane-exchange passes
     double2 *ULS, *WLS;       // [Nc][2][KS]
     double2 *UIN, *WIN;       // [Nc][2][KS]
     double *dcpart;           // [Nc]

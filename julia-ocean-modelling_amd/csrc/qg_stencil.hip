@@ -1124,8 +1124,8 @@ static int tend_slots(K kernel, int threads, int &sl) {
     return QG_OK;
 }
 
-// Default geometry: a whole number (QG_TEND_WAVES, default 2) of chip-fulls of strips (CUs x
-// resident workgroups per CU, from the occupancy API) -- a grid that is not a multiple leaves
+// Default geometry: a whole number of chip-fulls of strips (CUs x resident workgroups per
+// CU, from the occupancy API) -- a grid that is not a multiple leaves
 // a partly idle last "wave" of workgroups -- with rows split evenly over the strips and at
 // least 4 rows per strip.  (4096^2: 0.380 ms vs 0.385 for fixed 64-row strips; 1024^2: 33 vs
 // 38 us.)
@@ -1134,11 +1134,6 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     constexpr int TX = 256, PF = 1;  // register prefetch depth (rows)
     static int sl = 0;
     QG_CHECK(tend_slots(tendency_kernel<TX, PF, T>, TX, sl));
-    static int env_waves = -1;
-    if (env_waves < 0) {
-        const char *e = std::getenv("QG_TEND_WAVES");
-        env_waves = e ? std::max(1, std::atoi(e)) : 0;
-    }
     const int nx = (int)((a.M + TX - 1) / TX);
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
     // one chip-full of longer strips from ~1750^2 to ~3500^2 points: the ring prologue (6 rows
@@ -1152,7 +1147,7 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     // Since the scalar-unit cuts (r04) a strip's start costs less and shorter walks pay:
     // 4096^2 6 -> 9 chip-fulls 328 -> 323 us, 8192^2 12 -> 16 1 339 -> 1 317 us (6: 1 300 vs
     // 12: 1 267 on another box; tools/r04_p.sh, profiles/r04/waves/)
-    const int waves = env_waves ? env_waves : (pts >= 40.0e6 ? 16 : (pts >= 12.0e6 ? 9 : (pts >= 3.0e6 ? 1 : 2)));
+    const int waves = pts >= 40.0e6 ? 16 : (pts >= 12.0e6 ? 9 : (pts >= 3.0e6 ? 1 : 2));
     const int target = std::max(1, waves * sl / (2 * nx));  // row workgroups per column strip
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -1162,8 +1157,8 @@ static int launch_tend_balanced(const TendArgsT<T> &a, hipStream_t s) {
     return QG_OK;
 }
 
-// The certifying variant (PCG, one rank): both layers per workgroup, chip-fulls as above.
-// QG_CERT_TX = 128 / 256 (strip width), QG_CERT_WAVES = chip-fulls (tuning knobs).
+// The certifying variant (PCG, one rank): both layers per workgroup, 128-point strips (256:
+// 401 vs 398 us at 4096^2, same call), chip-fulls as above.
 template <int TX>
 static int launch_tendency_cert_t(const TendArgsT<double> &a, int64_t cap, int *nblk, hipStream_t s) {
     constexpr int PF = 1;
@@ -1174,20 +1169,12 @@ static int launch_tendency_cert_t(const TendArgsT<double> &a, int64_t cap, int *
         QG_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
         QG_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, tendency_kernel<TX, PF, double, true>, 2 * TX, 0));
         sl = cus * (per > 0 ? per : 1);
-        if (std::getenv("QG_CERT_VERBOSE")) std::fprintf(stderr, "cert tendency TX %d: %d resident\n", TX, sl);
     }
     const int nx = (int)((a.M + TX - 1) / TX);
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
-    const double pts = (double)a.M * (rA + rB);
-    static int ew = -1;
-    if (ew < 0) {
-        const char *e = std::getenv("QG_CERT_WAVES");
-        ew = e ? std::max(1, std::atoi(e)) : 0;
-    }
     // three chip-fulls (tools/sweep_r02g.sh, 4096^2 with the batched prologue: 2 -> 3
     // 388.8 -> 385.1 us, 2 to 8 within 2 %; before it 2 was best, tools/cert_sweep.sh)
-    (void)pts;
-    const int waves = ew ? ew : 3;
+    const int waves = 3;
     const int target = std::max(1, waves * sl / nx);
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
     const int nyA = split(rA), nyB = split(rB);
@@ -1205,18 +1192,16 @@ static int launch_tendency_cert_t(const TendArgsT<double> &a, int64_t cap, int *
 
 // up to ~1100^2 (128^2 13.6 -> 7.4 us, 1024^2 33.2 -> 31.2; 1536^2 slower)
 constexpr double TEND_DIRECT_PTS = 1.2e6;
-static int tend_direct_env();
 
 // below this many points per layer the certifying tendency is the cache-resident one-point
 // form (both layers per thread): 256^2 17.7 -> 13.9 us, 512^2 20.7 -> 18.7 us; at 1024^2 the
 // two-layer ring form is faster (40.6 vs 43.1 us), so the cut sits below the plain
-// tendency's TEND_DIRECT_PTS (QG_CERT_RING=1: always the ring form)
+// tendency's TEND_DIRECT_PTS.  qg_set_form(QG_FORM_TENDENCY, ...) forces either form.
 constexpr double CERT_DIRECT_PTS = 0.5e6;
 int launch_tendency_cert(const TendArgsT<double> &a, int64_t cap, int *nblk, hipStream_t s) {
     const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
-    const int de = tend_direct_env();
-    static const bool ring_only = std::getenv("QG_CERT_RING") != nullptr;  // (A/B: the ring form)
-    if ((de == 1 || (de < 0 && pts < CERT_DIRECT_PTS)) && !ring_only) {
+    const int f = form(QG_FORM_TENDENCY);
+    if (f == QG_TEND_DIRECT || (f != QG_TEND_RING && pts < CERT_DIRECT_PTS)) {
         const int nA = (a.j1 - a.j0 + 3) / 4, nB = a.j3 > a.j2 ? (a.j3 - a.j2 + 3) / 4 : 0;
         if (nA + nB == 0) {
             *nblk = 0;
@@ -1229,29 +1214,23 @@ int launch_tendency_cert(const TendArgsT<double> &a, int64_t cap, int *nblk, hip
         *nblk = (int)(grid.x * grid.y);
         return QG_OK;
     }
-    static int tx = -1;
-    if (tx < 0) {
-        const char *e = std::getenv("QG_CERT_TX");
-        tx = e ? std::atoi(e) : 128;  // (128 vs 256: 398 vs 401 us at 4096^2, same call)
-    }
-    return tx == 128 ? launch_tendency_cert_t<128>(a, cap, nblk, s) : launch_tendency_cert_t<256>(a, cap, nblk, s);
+    return launch_tendency_cert_t<128>(a, cap, nblk, s);
 }
 
 // Float32 default: the pair kernel over whole chip-fulls of 512-point strips (as above);
-// QG_TEND_PAIR=0 selects the one-point kernel instead.
+// qg_set_form(QG_FORM_TENDENCY, QG_TEND_ONE_POINT) selects the one-point kernel instead.
 template <int TX, class T>
 static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
     constexpr int W = 2 * TX, PF = 1;
     static int sl = 0;
     QG_CHECK(tend_slots(tendency_pair_kernel<TX, T, PF>, TX, sl));
-    const char *e = std::getenv("QG_TEND_WAVES");
     const int nx = (int)((a.M + W - 1) / W);
     const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
     // (tools/sweep_r02g.sh with the batched prologue: 8192^2 4 -> 6 chip-fulls 773 -> 764 us;
     // 4096^2 keeps 2: 209 vs 213-230 us.  r04, after the scalar-unit cuts: 8192^2 6 -> 12 -> 20
     // chip-fulls 652-719 -> 613-670 -> 646-652 us (12 -> 20 on one box: 663-668 -> 646-652),
     // tools/r04_p.sh, profiles/r04/waves/)
-    const int waves = e ? std::max(1, std::atoi(e)) : (pts >= 40.0e6 ? 20 : 2);
+    const int waves = pts >= 40.0e6 ? 20 : 2;
     const int rA = a.j1 - a.j0, rB = a.j3 > a.j2 ? a.j3 - a.j2 : 0;
     const int target = std::max(1, waves * sl / (2 * nx));
     auto split = [&](int rows) { return rows <= 0 ? 0 : std::max(1, std::min(rows / 4, (int)((int64_t)target * rows / (rA + rB)))); };
@@ -1262,39 +1241,14 @@ static int launch_tend_pair(const TendArgsT<T> &a, hipStream_t s) {
     return QG_OK;
 }
 
-static bool tend_pair_enabled() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = std::getenv("QG_TEND_PAIR");
-        v = e ? std::atoi(e) : 1;
-    }
-    return v != 0;
-}
-
-// Tile/pipeline variant (tuning knob; default 0).  QG_TEND_VARIANT selects it at run time.
-static int tend_variant() {
-    static int v = -1;
-    if (v < 0) {
-        const char *e = std::getenv("QG_TEND_VARIANT");
-        v = e ? std::atoi(e) : 0;
-    }
-    return v;
-}
-
-// Explicit tile (tuning knob / the LDS tile sweep of BASELINE config 3): QG_TEND_TILE="WxR"
-// = strips W points wide (one thread per point, W in {64, 128, 256, 512}) and about R rows per
-// workgroup.  0 = unset.
+// the strip tile of qg_set_form(QG_FORM_TENDENCY_TILE, (W << 16) | R): strips W points wide
+// (one thread per point, W in {64, 128, 256, 512}) and about R rows per workgroup -- BASELINE
+// config 3's LDS tile sweep.  w = 0: the default geometry.
 static void tend_tile(int &w, int &r) {
-    static int tw = -1, tr = 0;
-    if (tw < 0) {
-        tw = 0;
-        const char *e = std::getenv("QG_TEND_TILE");
-        if (e && std::sscanf(e, "%dx%d", &tw, &tr) != 2) tw = 0;
-        if (tw != 64 && tw != 128 && tw != 256 && tw != 512) tw = 0;
-        if (tr < 1) tw = 0;
-    }
-    w = tw;
-    r = tr;
+    const int v = form(QG_FORM_TENDENCY_TILE);
+    w = v >> 16;
+    r = v & 0xffff;
+    if ((w != 64 && w != 128 && w != 256 && w != 512) || r < 1) w = 0;
 }
 
 template <class T>
@@ -1304,16 +1258,6 @@ static int launch_tend_direct(const TendArgsT<T> &a, hipStream_t s) {
     tendency_direct_kernel<T><<<grid, 256, 0, s>>>(a, nA, nB);
     QG_LAUNCH_CHECK();
     return QG_OK;
-}
-
-// QG_TEND_DIRECT: 1 forces the cache-resident kernel, 0 the ring kernel; unset = by size
-static int tend_direct_env() {
-    static int v = -2;
-    if (v == -2) {
-        const char *e = std::getenv("QG_TEND_DIRECT");
-        v = e ? std::atoi(e) : -1;
-    }
-    return v;
 }
 
 template <class T>
@@ -1328,32 +1272,15 @@ static int launch_tendency_t(const TendArgsT<T> &a, hipStream_t s) {
         case 512: return launch_tend_variant<512, 1, T>(a, tr, s);
         default: break;
     }
+    const int f = form(QG_FORM_TENDENCY);
     if constexpr (sizeof(T) == 4) {
-        if (tend_variant() == 0 && tw == 0 && tend_pair_enabled() && a.M % 2 == 0) return launch_tend_pair<256>(a, s);
+        if (f == QG_TEND_AUTO && a.M % 2 == 0) return launch_tend_pair<256>(a, s);
     }  // (F64 pair kernel measured slower: 0.41-0.43 vs 0.386 ms at 4096^2 -- HBM-bound already)
-    if (tend_variant() == 0 && tw == 0) {
-        const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
-        const int de = tend_direct_env();
-        if (de == 1 || (de < 0 && pts < TEND_DIRECT_PTS)) return launch_tend_direct(a, s);
-        // ~870^2 .. ~1750^2 points: 128-wide strips of 8 rows (tile sweep: 1024^2 35 vs 38 us)
-        if (pts >= 0.75e6 && pts < 3.0e6) return launch_tend_variant<128, 1, T>(a, 8, s);
-    }
-    switch (tend_variant()) {
-        case 1: return launch_tend_variant<256, 1, T>(a, 32, s);
-        case 2: return launch_tend_variant<128, 1, T>(a, 64, s);
-        case 3: return launch_tend_variant<256, 1, T>(a, 128, s);
-        case 4: return launch_tend_variant<256, 2, T>(a, 64, s);
-        case 5: return launch_tend_variant<512, 1, T>(a, 64, s);
-        case 6: return launch_tend_variant<128, 2, T>(a, 64, s);
-        case 7: return launch_tend_variant<256, 3, T>(a, 64, s);
-        case 8: {  // r01 geometry: 64-row strips, fewer rows on small grids (>= 2048 workgroups)
-            const int64_t nx = (a.M + 255) / 256, rows_total = (a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0);
-            int rows = 64;
-            while (rows > 4 && nx * 2 * ((rows_total + rows - 1) / rows) < 2048) rows >>= 1;
-            return launch_tend_variant<256, 1, T>(a, rows, s);
-        }
-        default: return launch_tend_balanced(a, s);
-    }
+    const double pts = (double)a.M * ((a.j1 - a.j0) + (a.j3 > a.j2 ? a.j3 - a.j2 : 0));
+    if (f == QG_TEND_DIRECT || (f != QG_TEND_RING && pts < TEND_DIRECT_PTS)) return launch_tend_direct(a, s);
+    // ~870^2 .. ~1750^2 points: 128-wide strips of 8 rows (tile sweep: 1024^2 35 vs 38 us)
+    if (pts >= 0.75e6 && pts < 3.0e6) return launch_tend_variant<128, 1, T>(a, 8, s);
+    return launch_tend_balanced(a, s);
 }
 
 int launch_tendency(const TendArgsT<double> &a, hipStream_t s) { return launch_tendency_t(a, s); }

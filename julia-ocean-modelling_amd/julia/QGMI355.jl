@@ -24,7 +24,7 @@ module QGMI355
 using AMDGPU
 
 const libqg = get(ENV, "QGMI355_LIB", joinpath(@__DIR__, "..", "lib", "libqgmi355.so"))
-const ABI_VERSION = 4  # QG_ABI_VERSION of include/qg_mi355.h this binding was written against
+const ABI_VERSION = 5  # QG_ABI_VERSION of include/qg_mi355.h this binding was written against
 
 function __init__()
     v = ccall((:qg_abi_version, libqg), Cint, ())
@@ -236,6 +236,17 @@ end
 tendency runs (bit-identical; include/qg_mi355.h qg_set_overlap)."""
 set_overlap!(s::QGState, on::Bool=true) =
     @qgcheck qg_set_overlap ccall((:qg_set_overlap, libqg), Cint, (Ptr{Cvoid}, Cint), s.ctx, Cint(on))
+
+"""`set_form!(which, value)` / `get_form(which)`: process-wide kernel-form selection
+(include/qg_mi355.h qg_set_form; `which` = QG_FORM_*, value 0 = the automatic choice).  For
+checking alternative kernel forms against each other and for config 3's tile sweep."""
+set_form!(which::Integer, value::Integer) =
+    @qgcheck qg_set_form ccall((:qg_set_form, libqg), Cint, (Cint, Cint), Cint(which), Cint(value))
+function get_form(which::Integer)
+    v = ccall((:qg_get_form, libqg), Cint, (Cint,), Cint(which))
+    v < 0 && error("QGMI355: qg_get_form($which) failed with status $v")
+    Int(v)
+end
 
 """`set_halo_transport!(s, mode)`: collective; `mode` = `:rccl` (send/recv), `:peer` (copy engine into the
 neighbours' IPC-mapped regions) or `:put` (one small kernel storing into them) -- include/qg_mi355.h

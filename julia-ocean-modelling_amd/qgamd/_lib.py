@@ -21,6 +21,9 @@ QG_F64, QG_F32 = 0, 1
 QG_SOLVER_PCG = 1
 QG_PRECOND_NONE = 0
 QG_PRECOND_SPECTRAL = 1
+# qg_set_form (kernel-form selection, process-wide; 0 = automatic)
+QG_FORM_TENDENCY, QG_FORM_TENDENCY_TILE, QG_FORM_ROW_SPLIT, QG_FORM_PCG_NO_CERTIFICATE = 0, 1, 2, 3
+QG_TEND_AUTO, QG_TEND_RING, QG_TEND_DIRECT, QG_TEND_ONE_POINT = 0, 1, 2, 3
 
 
 class QgParams(C.Structure):
@@ -100,6 +103,8 @@ SIGNATURES = [
                                    C.POINTER(_vp)]),
     ("qg_solver_solve", C.c_int, [_vp, _dp, _dp, _dp, _dp]),
     ("qg_solver_destroy", C.c_int, [_vp]),
+    ("qg_set_form", C.c_int, [C.c_int, C.c_int]),
+    ("qg_get_form", C.c_int, [C.c_int]),
     ("qg_laplace_5p", C.c_int, [_dp, _dp, _i64, _i64, C.c_double, _vp]),
     ("qg_cd", C.c_int, [_dp, _dp, _i64, _i64, C.c_double, _vp]),
     ("qg_arakawa_J", C.c_int, [_dp, _dp, _dp, _i64, _i64, C.c_double, _vp]),
@@ -132,6 +137,9 @@ def lib():
             pass
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
+            # (an older experiment build named by QGMI355_LIB may lack newer entry points)
+            if os.environ.get("QGMI355_LIB") and not hasattr(L, name):
+                continue
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

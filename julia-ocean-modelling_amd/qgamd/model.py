@@ -20,6 +20,7 @@ cannot carry ``!``; the mutating functions end in ``_`` instead.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from dataclasses import dataclass, field
 
@@ -35,6 +36,32 @@ YEAR = 60 * 60 * 24 * 365
 
 SEED_LAYER1 = 20241008
 SEED_LAYER2 = 20241009
+
+
+# ---------------------------------------------------------------------------------------
+# kernel-form selection (qg_set_form: process-wide, 0 = the library's choice by size)
+# ---------------------------------------------------------------------------------------
+def set_form(which, value):
+    """Force one kernel form (``_lib.QG_FORM_*``); value 0 restores the automatic choice."""
+    call("qg_set_form", int(which), int(value))
+
+
+def get_form(which):
+    v = _lib.lib().qg_get_form(int(which))
+    if v < 0:
+        raise _lib.QGError("qg_get_form", v)
+    return v
+
+
+@contextlib.contextmanager
+def forced_form(which, value):
+    """``with forced_form(QG_FORM_TENDENCY, QG_TEND_RING): ...`` -- the previous value after."""
+    old = get_form(which)
+    set_form(which, value)
+    try:
+        yield
+    finally:
+        set_form(which, old)
 
 
 # ---------------------------------------------------------------------------------------

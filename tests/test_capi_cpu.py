@@ -37,7 +37,7 @@ def test_exports_every_declared_symbol(qglib):
 
 
 def test_abi_version_and_strerror(qglib):
-    assert qglib.qg_abi_version() == 4
+    assert qglib.qg_abi_version() == 5
     assert qglib.qg_strerror(0) == b"ok"
     assert b"unsupported" in qglib.qg_strerror(-2)
 
@@ -187,3 +187,30 @@ def test_missing_library_fails_loudly(tmp_path):
     env = dict(os.environ, QGMI355_LIB=str(tmp_path / "absent.so"))
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert "RAISED True" in r.stdout, (r.stdout, r.stderr)
+
+
+def test_form_api_validates(qglib):
+    """qg_set_form / qg_get_form (pure host state, no device): range checks, round trip."""
+    import qgamd as qg
+    L = qg._lib
+    assert qg.get_form(L.QG_FORM_TENDENCY) == 0
+    for which, bad in ((L.QG_FORM_TENDENCY, 4), (L.QG_FORM_ROW_SPLIT, 2), (L.QG_FORM_PCG_NO_CERTIFICATE, 2),
+                       (L.QG_FORM_TENDENCY_TILE, (100 << 16) | 4), (L.QG_FORM_TENDENCY_TILE, 256 << 16), (99, 0),
+                       (L.QG_FORM_TENDENCY, -1)):
+        with pytest.raises(qg.QGError):
+            qg.set_form(which, bad)
+    with qg.forced_form(L.QG_FORM_TENDENCY_TILE, (128 << 16) | 8):
+        assert qg.get_form(L.QG_FORM_TENDENCY_TILE) == (128 << 16) | 8
+    assert qg.get_form(L.QG_FORM_TENDENCY_TILE) == 0
+    assert qglib.qg_get_form(17) == L.QG_ERR_INVALID_ARG
+
+
+def test_library_reads_only_documented_switches():
+    """The shipped library reads only the documented environment switches (QG_OVERLAP,
+    QG_GRAPH, QG_HALO_PEER, QG_GATHER_PEER, QG_COMM_TIMEOUT); kernel-form choices go through
+    qg_set_form."""
+    src = os.path.join(PKG, "csrc")
+    found = set()
+    for f in os.listdir(src):
+        found |= set(re.findall(r'getenv\("(\w+)"\)', open(os.path.join(src, f)).read()))
+    assert found == {"QG_OVERLAP", "QG_GRAPH", "QG_HALO_PEER", "QG_GATHER_PEER", "QG_COMM_TIMEOUT"}, found

@@ -241,3 +241,20 @@ def test_reference_signatures_slot1(qg):
     finally:
         qg.set_dropin_slots("all")
         qg.unbind(zeta, psi, f_store)
+
+
+def test_keep_order_slot1_to_full_refused(qg):
+    """Lean mode leaves slots 2-3 of zeta / psi stale, so a direct switch to full keep-order
+    (which promises store_new_state!'s slots after every call) is refused; via the rotating
+    mode (0) it is allowed, and canonicalizes."""
+    m = qg.bench_model(64)
+    st = qg.initialise_model(m)
+    st.set_keep_order(True, slot1_only=True)
+    st.run(1, 3)
+    with pytest.raises(qg.QGError) as e:
+        st.set_keep_order(True)
+    assert e.value.status == qg._lib.QG_ERR_INVALID_ARG
+    st.set_keep_order(False)
+    st.set_keep_order(True)
+    st.run(4, 2)
+    assert st.heads() == [0, 0, 0]

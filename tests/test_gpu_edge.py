@@ -123,14 +123,14 @@ def test_split_rows_beyond_generic(env, M, P, steps):
 
 
 @pytest.mark.parametrize("M,P", [(3000, 24), (1001, 16), (45, 40), (120, 16), (2310, 12)])
-def test_split_passes_match_generic(env, M, P, monkeypatch):
-    """QG_SPLIT_FORCE routes generic-size rows through the split passes: same answer as the
-    generic passes (different FFT order: roundoff only) and the oracle."""
+def test_split_passes_match_generic(env, M, P):
+    """qg_set_form(QG_FORM_ROW_SPLIT, 1) routes generic-size rows through the split passes:
+    same answer as the generic passes (different FFT order: roundoff only) and the oracle."""
     qg, O, R = env
     m = qg.bench_model(M, P=P, dt=600.0)
     gen = qg.run_model_no_output(m, nsteps=4)
-    monkeypatch.setenv("QG_SPLIT_FORCE", "1")
-    spl = qg.run_model_no_output(m, nsteps=4)
+    with qg.forced_form(qg._lib.QG_FORM_ROW_SPLIT, 1):
+        spl = qg.run_model_no_output(m, nsteps=4)
     ref = O.State(R.bench_model(M, P=P, dt=600.0)).run(4)
     for n in ("psi", "zeta", "f_store"):
         err = rel(spl.to_numpy(n), gen.to_numpy(n))

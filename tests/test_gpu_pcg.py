@@ -86,12 +86,12 @@ def test_certification_failure_restarts_from_z0(env):
     assert np.linalg.norm(st.to_numpy("psi") - ref.psi) / np.linalg.norm(ref.psi) < 1e-10
 
 
-def test_alpha_iteration_path(env, monkeypatch):
-    """QG_PCG_NOCERT: the fused alpha iteration (z0, alpha = (b,z0)/(z0,Bz0), psi = P(alpha z0))
-    that serves non-invertible back-projections; same answer."""
+def test_alpha_iteration_path(env):
+    """qg_set_form(QG_FORM_PCG_NO_CERTIFICATE, 1): the fused alpha iteration (z0, alpha =
+    (b,z0)/(z0,Bz0), psi = P(alpha z0)) that serves non-invertible back-projections; same answer."""
     torch, qg, R, O = env
-    monkeypatch.setenv("QG_PCG_NOCERT", "1")
-    st = qg.run_model_no_output(qg.bench_model(64), nsteps=6, solver=1)
+    with qg.forced_form(qg._lib.QG_FORM_PCG_NO_CERTIFICATE, 1):
+        st = qg.run_model_no_output(qg.bench_model(64), nsteps=6, solver=1)
     s = st.stats()
     assert s["iters"][0] == 1 and max(s["relres"]) < 1e-13
     ref = O.State(R.bench_model(64)).run(6)

@@ -1,42 +1,36 @@
 """The two tendency kernels (the LDS-ring kernel for large grids, the cache-resident one for
 grids below ~1.2 M points, csrc/qg_stencil.hip) evaluate the same expressions in the same
-order: forced one way and the other (QG_TEND_DIRECT, read once per process, hence one
-subprocess each), five Euler + AB3 steps give bit-identical states, on a square grid and on
-a ragged one (odd P, M not a multiple of the 64-point tile)."""
+order: forced one way and the other (qg_set_form(QG_FORM_TENDENCY, QG_TEND_RING / _DIRECT)),
+five Euler + AB3 steps give bit-identical states, on a square grid and on a ragged one (odd P,
+M not a multiple of the 64-point tile); the same for the certifying tendency of the PCG solver."""
 import hashlib
 import os
-import subprocess
 import sys
 
 import pytest
 
 pytestmark = pytest.mark.gpu
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-
-SCRIPT = r"""
-import hashlib, sys
-sys.path[:0] = [sys.argv[1], sys.argv[1] + "/julia-ocean-modelling_amd"]
-import torch, qgamd
-M, P = int(sys.argv[2]), int(sys.argv[3])
-st = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=5)
-h = hashlib.sha1()
-for n in ("zeta", "psi", "f_store"):
-    h.update(st.to_numpy(n).tobytes())
-print(h.hexdigest())
-"""
+sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
 
 
-def _run(direct, M, P):
-    env = dict(os.environ, QG_TEND_DIRECT=str(direct))
-    r = subprocess.run([sys.executable, "-c", SCRIPT, ROOT, str(M), str(P)], env=env, capture_output=True,
-                       text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-2000:]
-    return r.stdout.strip().splitlines()[-1]
+def _run(qg, form, M, P, solver):
+    with qg.forced_form(qg._lib.QG_FORM_TENDENCY, form):
+        st = qg.run_model_no_output(qg.bench_model(M, P=P), nsteps=5, solver=solver)
+        h = hashlib.sha1()
+        for n in ("zeta", "psi", "f_store"):
+            h.update(st.to_numpy(n).tobytes())
+        st.close()
+    return h.hexdigest()
 
 
+@pytest.mark.parametrize("solver", [0, 1])
 @pytest.mark.parametrize("M,P", [(256, 256), (200, 37)])
-def test_ring_and_direct_tendency_kernels_bitwise(M, P):
+def test_ring_and_direct_tendency_kernels_bitwise(M, P, solver):
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    assert _run(0, M, P) == _run(1, M, P)
+    import qgamd as qg
+    assert _run(qg, qg._lib.QG_TEND_RING, M, P, solver) == _run(qg, qg._lib.QG_TEND_DIRECT, M, P, solver)
+

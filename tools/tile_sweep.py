@@ -1,6 +1,6 @@
 """LDS tile sweep of the tendency kernel (BASELINE config 3: 4096^2 F64, one MI355X).
 
-For each tile W x R (strip width W threads/points, ~R rows per workgroup; QG_TEND_TILE) and
+For each tile W x R (strip width W threads/points, ~R rows per workgroup; qg_set_form(QG_FORM_TENDENCY_TILE)) and
 the default geometry, runs tools/tune_tend.py in a fresh process (HIP-event times of 20
 qg_evolve_zeta / qg_evolve_psi launches after 5 warm-up steps) and checks that every tile
 produced bit-identical zeta (the tiling only changes the traversal).  Writes one JSON list.
@@ -21,11 +21,7 @@ def main():
     tiles = sys.argv[3].split(",") if len(sys.argv) > 3 else TILES
     rows = []
     for tile in [None] + tiles:
-        env = dict(os.environ)
-        env.pop("QG_TEND_TILE", None)
-        if tile:
-            env["QG_TEND_TILE"] = tile
-        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tune_tend.py"), n], env=env,
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "tune_tend.py"), n] + ([tile] if tile else []),
                            capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
             print(r.stderr[-2000:], file=sys.stderr)
