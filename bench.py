@@ -84,23 +84,31 @@ def parse():
                          "RCCL's network transport over loopback carries the halo send/recv and the "
                          "all-gathers -- a rehearsal of the multi-GPU code path on a one-GPU box (not "
                          "xGMI, not a measurement)")
-    ap.add_argument("--overlap", dest="overlap", action="store_true", default=True,
+    ap.add_argument("--overlap", dest="overlap", action="store_true", default=None,
                     help="N > 1 (or --comm-self): post the halo exchange on a second stream while the "
-                         "interior rows' tendency runs (qg_set_overlap; bit-identical results; the default)")
+                         "interior rows' tendency runs (qg_set_overlap; bit-identical results).  Default: "
+                         "on for the RCCL and copy-engine halos, off for the put halo (its 10 us kernel "
+                         "beats splitting the tendency, r04v)")
     ap.add_argument("--no-overlap", dest="overlap", action="store_false",
                     help="N > 1 (or --comm-self): the exchange in stream order before the whole tendency")
-    ap.add_argument("--halo", choices=["rccl", "peer", "put"], default="rccl",
+    ap.add_argument("--halo", choices=["auto", "rccl", "peer", "put"], default="auto",
                     help="RCCL transport: how the halo rows travel (qg_comm_set_halo_transport): rccl = "
                          "pack + grouped send/recv; peer = copy-engine copies into the neighbours' "
                          "IPC-mapped receive regions + arrival flags; put = the same regions, rows stored "
-                         "by one small kernel")
-    ap.add_argument("--gather", choices=["rccl", "peer"], default="rccl",
+                         "by one small kernel; auto (default) = put when the IPC regions can be set up on "
+                         "every rank (collective, all-or-nothing), else rccl -- the choice is in config")
+    ap.add_argument("--gather", choices=["auto", "rccl", "peer"], default="auto",
                     help="RCCL transport, direct solver: how the per-step record all-gather travels "
                          "(qg_comm_set_gather_transport): rccl = ncclAllGather; peer = one kernel storing "
-                         "into every peer's IPC-mapped region")
+                         "into every peer's IPC-mapped region; auto (default) = peer when the regions can "
+                         "be set up on every rank, else rccl")
     ap.add_argument("--no-transport-ab", dest="transport_ab", action="store_false", default=True,
-                    help="N > 1 (or --comm-self): skip re-timing the K steps with the other halo / gather "
-                         "transports (transport_ab)")
+                    help="N > 1 (or --comm-self): skip re-timing the K steps with RCCL's halo and gather "
+                         "when the headline ran the peer transports (transport_ab)")
+    ap.add_argument("--transport-ab-peer", action="store_true",
+                    help="N > 1 (or --comm-self) with an RCCL headline: re-time the K steps with the peer "
+                         "transports after the headline (opt-in: a fault in that leg would lose the "
+                         "headline line)")
     ap.add_argument("--dropin-steps", type=int, default=20,
                     help="also time this many steps through the reference's own array signatures "
                          "(evolve_zeta!(model, zeta, psi, t, f_store) / evolve_psi!(...) on bare arrays, "
@@ -112,6 +120,30 @@ def parse():
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
     return ap.parse_args()
+
+
+def choose_transports(qgamd, st, halo, gather, spectral):
+    """Halo / record-gather transports of an RCCL run (collective: every rank calls it with the
+    same arguments).  "auto" takes the peer transports (put halo, peer gather) when the IPC
+    regions can be set up on every rank -- the library's set-up is all-or-nothing, the same
+    verdict on every rank (QG_ERR_UNSUPPORTED) -- else RCCL.  Returns the choice, for config."""
+    want_peer_gather = spectral and gather in ("auto", "peer")
+    want_halo = "put" if halo == "auto" else halo
+    try:
+        if want_peer_gather:
+            st.set_gather_transport("peer")
+        if want_halo != "rccl":
+            st.set_halo_transport(want_halo)
+    except qgamd.QGError as e:
+        if e.status != qgamd._lib.QG_ERR_UNSUPPORTED or "auto" not in (halo, gather):
+            raise
+        # (unavailable on some rank: every rank got the same verdict and stays on RCCL)
+        if getattr(st, "gather_transport", "rccl") != "rccl":
+            st.set_gather_transport("rccl")
+        return f"rccl: peer regions unavailable ({e})"
+    if "auto" in (halo, gather):
+        return "auto: peer regions set up on every rank"
+    return "as requested"
 
 
 def _cpu_model():
@@ -379,14 +411,13 @@ def main():
             uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         st.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
-    if args.halo != "rccl" and args.transport == "rccl" and (world > 1 or args.comm_self):
-        st.set_halo_transport(args.halo)
-    if args.gather != "rccl" and args.transport == "rccl" and (world > 1 or args.comm_self) \
-            and args.solver == "spectral":
-        st.set_gather_transport(args.gather)
-    st.set_overlap(args.overlap)
+    transport_choice = None
+    if args.transport == "rccl" and (world > 1 or args.comm_self):
+        transport_choice = choose_transports(qgamd, st, args.halo, args.gather, args.solver == "spectral")
     cur_halo = getattr(st, "halo_transport", "rccl")
     cur_gather = getattr(st, "gather_transport", "rccl")
+    overlap = args.overlap if args.overlap is not None else cur_halo != "put"
+    st.set_overlap(overlap)
     st.initialise()
     torch.cuda.synchronize()
     setup_ms = (time.perf_counter() - t_setup) * 1e3
@@ -504,7 +535,7 @@ def main():
                                      + comm.get("allgather_ms_max_over_ranks", comm["allgather_ms"])) / (el * 1e3 / K)
             err2, el2 = None, None
             try:
-                st.set_overlap(not args.overlap)
+                st.set_overlap(not overlap)
                 for _ in range(3):
                     st.step(t)
                     t += 1
@@ -516,7 +547,7 @@ def main():
                 torch.cuda.synchronize()
                 el2 = time.perf_counter() - t1
                 t += K
-                st.set_overlap(args.overlap)
+                st.set_overlap(overlap)
             except Exception as e:  # noqa: BLE001
                 err2 = f"{type(e).__name__}: {e}"
             if all_ok(err2 is None):
@@ -524,7 +555,7 @@ def main():
                     tt = torch.tensor([el2], dtype=torch.float64, device=dev_red)
                     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
                     el2 = float(tt.item())
-                overlap_ab = {"halo_overlap": not args.overlap, "value": world * K / el2,
+                overlap_ab = {"halo_overlap": not overlap, "value": world * K / el2,
                               "ms_per_step": el2 * 1e3 / K, "steps": K,
                               "note": "the same K steps re-timed in this invocation with qg_set_overlap "
                                       "toggled (the headline value uses halo_overlap of config)"}
@@ -534,15 +565,16 @@ def main():
             comm = {"error": err or "failed on another rank"}
             overlap_ab = {"error": "skipped: the comm probe failed"}
 
-    # the same K steps with the other halo / gather transports (RCCL <-> peer copies), after the
-    # headline: a failure here (e.g. IPC unavailable between the GPUs) is reported, not fatal
+    # the same K steps with the other halo / gather transports, after the headline: a peer
+    # headline -> RCCL with the overlap on (by default); an RCCL headline -> the peer transports
+    # in their best measured schedule (put halo + peer gather, overlap off; opt-in with
+    # --transport-ab-peer: a fault in an untried transport after the headline would lose the
+    # headline line).  An error here is reported, not fatal.
     transport_ab = None
+    peer_now = (cur_halo, cur_gather) != ("rccl", "rccl")
     if args.transport_ab and args.transport == "rccl" and (world > 1 or args.comm_self) \
-            and args.solver == "spectral" and args.comm_probe_reps > 0:
-        # RCCL headline -> the peer transports in their best measured schedule (put halo +
-        # peer gather, overlap off: the 10 us put beats splitting the tendency, r04v); a peer
-        # headline -> RCCL with the overlap on
-        peer_now = (cur_halo, cur_gather) != ("rccl", "rccl")
+            and args.solver == "spectral" and args.comm_probe_reps > 0 \
+            and (peer_now or (args.transport_ab_peer and not (transport_choice or "").startswith("rccl: peer"))):
         alt_h, alt_g, alt_ov = ("rccl", "rccl", True) if peer_now else ("put", "peer", False)
         err3, el3 = None, None
         import ctypes as C
@@ -629,7 +661,8 @@ def main():
             "transport": (("rccl, all ranks on one GPU: network transport over loopback (--one-gpu rehearsal, "
                            "not xGMI, not a measurement)" if one_gpu else args.transport)
                           if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
-            "halo_overlap": bool(args.overlap and (world > 1 or args.comm_self)),
+            "halo_overlap": bool(overlap and (world > 1 or args.comm_self)),
+            "transport_choice": transport_choice,
             "halo_transport": (cur_halo if args.transport == "rccl" and (world > 1 or args.comm_self) else None),
             "gather_transport": (cur_gather if args.transport == "rccl" and (world > 1 or args.comm_self)
                                  and args.solver == "spectral" else None),

@@ -65,8 +65,9 @@ typedef enum {
 
 typedef enum {
     QG_SOLVER_SPECTRAL = 0, /* direct: x-DFT + parallel cyclic tridiagonal solve in y;    *
-                             * any M in 3..8192 and even M up to 16384 (M = 2^k: FFT      *
-                             * passes), else UNSUPPORTED                                  */
+                             * any M in 3..262144 (M = 2^k <= 8192: FFT passes; odd M     *
+                             * above 8192 and M above 16384: Bluestein row transforms),   *
+                             * P >= 2, else UNSUPPORTED                                   */
     QG_SOLVER_PCG = 1       /* matrix-free PCG on the 5-point operator                     */
 } qg_solver_kind;
 
@@ -157,8 +158,11 @@ int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2
  * on = QG_KEEP_ORDER_SLOT1 (2): slot 1 of zeta and psi and all three slots of f_store as
  * above after every call, slots 2-3 of zeta and psi NOT maintained -- the reference never
  * reads them (only evolve_zeta_layer! reads f_store's history), so its loop computes the
- * same values: no shifts of zeta and psi, the new zeta written to slot 2 and copied to slot 1
- * (one slot copy per step instead of four).  Switching from QG_KEEP_ORDER_SLOT1 straight to
+ * same values: no shifts of zeta and psi, the new zeta written to slot 2 and moved to slot 1
+ * by the next qg_evolve_psi's first solver pass, which reads it anyway (spectral solver, power-
+ * of-two M, one rank; else a slot copy at the end of qg_evolve_zeta).  Until that solve,
+ * qg_slot(ctx, 0, 1, ..) names slot 2 as the newest zeta; qg_evolve_zeta, qg_synchronize,
+ * qg_canonicalize and every call that moves or rebinds slots complete the move first.  Switching from QG_KEEP_ORDER_SLOT1 straight to
  * on = 1 returns QG_ERR_INVALID_ARG (slots 2-3 of zeta and psi hold stale values then).      */
 #define QG_KEEP_ORDER_SLOT1 2
 int qg_set_keep_order(qg_ctx *ctx, int on);

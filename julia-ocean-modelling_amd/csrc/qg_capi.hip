@@ -96,6 +96,10 @@ struct qg_ctx {
     // which the reference never reads, are not maintained (no shifts of zeta and psi; the new
     // zeta goes through slot 2, one slot copy)
     int keep_order = 0;
+    // lean mode, single GPU, spectral solver: the new zeta waits in slot 2 (heads[0] = 1) and
+    // the next solve's pass A, which reads it anyway, writes it into slot 1 (settle_zcopy when
+    // anything else comes first)
+    bool zcopy_pending = false;
     bool capturing = false;  // a step graph is being captured (no host reads, no polls)
     // deferred PCG: the latch is copied to page-locked memory every QG_PACE_STEPS steps and
     // read one interval later without blocking, so a failed certificate stops qg_step /
@@ -259,9 +263,14 @@ int qg_create(const qg_params *p, int device, void *stream, qg_ctx **out) {
     return QG_OK;
 }
 
+static int settle_zcopy(qg_ctx *c);
+
 int qg_destroy(qg_ctx *c) {
     if (!c) return QG_OK;
     (void)hipSetDevice(c->device);
+    // the caller's arrays outlive the context: a pending lean-mode move completes first (in
+    // stream order; the caller synchronises its stream before reading them)
+    if (c->zeta) (void)settle_zcopy(c);
     if (c->snap_stream) (void)hipStreamSynchronize(c->snap_stream);
     if (c->snap) (void)hipFree(c->snap);
     if (c->snap_ready) (void)hipEventDestroy(c->snap_ready);
@@ -297,12 +306,26 @@ static int settle_pcg(qg_ctx *c) {
     return c->pcg->certify_pending(c->stream, c->distributed ? comm_allgather : nullptr, c->comm);
 }
 
+// Lean keep-order mode: complete a pending move of the new zeta into slot 1 (the solve's pass A
+// did not run since the tendency; slots 2-3 of zeta are not maintained in this mode).
+static int settle_zcopy(qg_ctx *c) {
+    if (!c->zcopy_pending) return QG_OK;
+    static const int mv[1][3] = {{1, -1, -1}};
+    void *arr[1] = {c->zeta};
+    QG_HIP(hipSetDevice(c->device));
+    QG_CHECK(launch_slot_move(arr, mv, 1, 2 * c->esize * c->F, c->stream));
+    c->heads[0] = 0;
+    c->zcopy_pending = false;
+    return QG_OK;
+}
+
 // (the arrays bound before must still be valid here: a pending certification reads them)
 int qg_bind_state(qg_ctx *c, void *zeta, void *psi, void *f_store) {
     if (!c || !zeta || !psi || !f_store) return QG_ERR_INVALID_ARG;
     for (const void *b : {zeta, psi, f_store})  // (launch_slot_move's 16-byte vectors)
         if (reinterpret_cast<uintptr_t>(b) % 16 != 0) return QG_ERR_INVALID_ARG;
     if (c->zeta) QG_CHECK(settle_pcg(c));
+    if (c->zeta) QG_CHECK(settle_zcopy(c));
     drop_graphs(c);
     c->zeta = zeta;
     c->psi = psi;
@@ -324,6 +347,7 @@ int qg_initialise(qg_ctx *c, uint64_t seed1, uint64_t seed2) {
                                       (int64_t)c->rank * p.P, amp, c->d.S1, c->d.S2, p.dx, seed1, seed2,
                                       c->stream));
     c->heads[0] = c->heads[1] = c->heads[2] = 0;
+    c->zcopy_pending = false;  // (every slot rewritten)
     c->initialised = true;
     c->seeded_rank = c->rank;
     c->seeded_nranks = c->nranks;
@@ -342,6 +366,7 @@ int qg_set_slots(qg_ctx *c, const int heads[3]) {
         if (heads[k] < 0 || heads[k] > 2) return QG_ERR_INVALID_ARG;
     if (c->keep_order && (heads[0] || heads[1] || heads[2])) return QG_ERR_INVALID_ARG;
     QG_CHECK(settle_pcg(c));
+    QG_CHECK(settle_zcopy(c));
     for (int k = 0; k < 3; ++k) c->heads[k] = heads[k];
     return QG_OK;
 }
@@ -399,6 +424,7 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     // overwritten in place
     const bool fuse_fshift = c->keep_order && !c->distributed && timestep >= 3;
     const bool lean = c->keep_order == QG_KEEP_ORDER_SLOT1;
+    QG_CHECK(settle_zcopy(c));  // (two tendencies in a row: the first one's zeta into slot 1 now)
     if (c->keep_order && !lean) {
         void *arr[2] = {c->zeta, c->fst};
         QG_CHECK(launch_slot_shift(arr, fuse_fshift ? 1 : 2, 2 * c->esize * c->F, c->stream));
@@ -511,11 +537,19 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
         }
         c->ghosts_pending = true;
     }
-    if (lean) {  // slot 1 <- slot 2 (ghost rows too; multi-rank: refreshed by the lazy flush)
-        static const int mv[1][3] = {{1, -1, -1}};
-        void *arr[1] = {c->zeta};
-        QG_CHECK(launch_slot_move(arr, mv, 1, 2 * c->esize * c->F, c->stream));
-        zn = 0;
+    if (lean) {
+        if (c->spec && !c->distributed && c->spec->fuses_input_copy()) {
+            // the next solve's pass A reads the new zeta from slot 2 and writes it into slot 1
+            // (stores only; r04n's separate move read and wrote the whole field, ~0.09 ms at
+            // 4096^2); meanwhile qg_slot names slot 2 as the newest
+            zn = 1;
+            c->zcopy_pending = true;
+        } else {  // slot 1 <- slot 2 (ghost rows too; multi-rank: refreshed by the lazy flush)
+            static const int mv[1][3] = {{1, -1, -1}};
+            void *arr[1] = {c->zeta};
+            QG_CHECK(launch_slot_move(arr, mv, 1, 2 * c->esize * c->F, c->stream));
+            zn = 0;
+        }
     }
     c->heads[0] = zn;
     c->heads[2] = fn;
@@ -601,8 +635,17 @@ int qg_evolve_psi(qg_ctx *c) {
         c->last_status = st;
         if (st != QG_OK && st != QG_ERR_NOT_CONVERGED) return st;
     } else {
+        void *zc1 = nullptr, *zc2 = nullptr;
+        if (c->zcopy_pending) {  // pass A also moves the new zeta (slot 2) into slot 1
+            zc1 = c->field(c->zeta, 0, 0);
+            zc2 = c->field(c->zeta, 1, 0);
+        }
         QG_CHECK(c->spec->solve(z1, z2, o1, o2, !c->distributed, c->stream,
-                                c->distributed ? comm_gather_records : nullptr, c->comm));
+                                c->distributed ? comm_gather_records : nullptr, c->comm, nullptr, nullptr, zc1, zc2));
+        if (c->zcopy_pending) {
+            c->heads[0] = 0;
+            c->zcopy_pending = false;
+        }
     }
     c->heads[1] = pn;
     if (c->distributed) c->ghosts_pending = true;  // psi's ghost rows: at the next ghost flush
@@ -723,6 +766,7 @@ int qg_canonicalize(qg_ctx *c) {
     QG_HIP(hipSetDevice(c->device));
     QG_CHECK(flush_ghosts(c));  // pending ghost-ring refreshes
     QG_CHECK(settle_pcg(c));    // (its check reads the slots about to move)
+    QG_CHECK(settle_zcopy(c));
     // one launch rotates every field whose newest slot is not physical 0: new slot q <- old
     // slot (head + q) mod 3, each slot read once and written once, in place
     void *arr[3];
@@ -744,6 +788,7 @@ int qg_set_keep_order(qg_ctx *c, int on) {
     // slots 2-3 of zeta and psi were not maintained in the lean mode: full keep-order could
     // not keep its promise for the next two calls
     if (on == 1 && c->keep_order == QG_KEEP_ORDER_SLOT1) return QG_ERR_INVALID_ARG;
+    QG_CHECK(settle_zcopy(c));
     if (on && !c->keep_order && c->zeta) QG_CHECK(qg_canonicalize(c));
     if (c->keep_order != on) drop_graphs(c);
     c->keep_order = on;
@@ -886,6 +931,7 @@ int qg_synchronize(qg_ctx *c) {
     if (!c) return QG_ERR_INVALID_ARG;
     QG_HIP(hipSetDevice(c->device));
     QG_CHECK(flush_ghosts(c));
+    QG_CHECK(settle_zcopy(c));
     if (c->pcg && c->pcg->deferred()) {  // deferred PCG: new certification failures?
         QG_CHECK(c->pcg->certify_pending(c->stream, c->distributed ? comm_allgather : nullptr, c->comm));
         double lt[8];
@@ -967,6 +1013,7 @@ int qg_comm_init(qg_ctx *c, int nranks, int rank, const char id[128]) {
     if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return QG_ERR_INVALID_ARG;
     if (seeded_for_other_slab(c, nranks, rank)) return QG_ERR_INVALID_ARG;
     QG_CHECK(settle_pcg(c));  // (the solver is rebuilt)
+    if (c->zeta) QG_CHECK(settle_zcopy(c));
     QG_HIP(hipSetDevice(c->device));
     if (c->comm) {
         comm_destroy(c->comm);
@@ -1018,6 +1065,7 @@ int qg_comm_init_host(qg_ctx *c, int nranks, int rank, qg_allgather_fn allgather
     if (!c || nranks < 1 || rank < 0 || rank >= nranks || !allgather || !sendrecv) return QG_ERR_INVALID_ARG;
     if (seeded_for_other_slab(c, nranks, rank)) return QG_ERR_INVALID_ARG;
     QG_CHECK(settle_pcg(c));  // (the solver is rebuilt)
+    if (c->zeta) QG_CHECK(settle_zcopy(c));
     QG_HIP(hipSetDevice(c->device));
     if (c->comm) {
         comm_destroy(c->comm);

@@ -137,6 +137,22 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
         }
     };
     constexpr bool PF = N < 8192;  // (N = 8192: no register prefetch, registers are short)
+    // the drop-in lean mode: row j of the inputs also goes to zcopy (ghost ring included),
+    // from the registers the projection reads -- stores only, no extra reads
+    auto copy_row = [&](int j, auto &d1, auto &d2) {
+        S *o1 = static_cast<S *>(a.zcopy1) + (size_t)(j + 1) * ld, *o2 = static_cast<S *>(a.zcopy2) + (size_t)(j + 1) * ld;
+        S *g1 = ghost_row_target(static_cast<S *>(a.zcopy1), ld, a.P, j, true);
+        S *g2 = ghost_row_target(static_cast<S *>(a.zcopy2), ld, a.P, j, true);
+#pragma unroll
+        for (int p = 0; p < EP; ++p) {
+            const int i = t + p * T;
+            if (N % T == 0 || i < N) {
+                store_row_with_ghosts(o1, g1, N, i, d1[p]);
+                store_row_with_ghosts(o2, g2, N, i, d2[p]);
+            }
+        }
+    };
+    const bool zcopy = a.zcopy1 != nullptr;
     // r of this thread's lines, loaded once: row-invariant, and at this kernel's register
     // budget (224 VGPRs before at 4096) the values fit without spilling, so no row reloads
     // them from L2 (below 1024 no gain measured)
@@ -169,6 +185,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                 else if (NH % T == 0 || k < NH) rq[q][s] = QG_CR(s * KS + k);
             }
 #define QG_PA_R(q, s, o) rq[q][s]
+        if (zcopy) copy_row(j, c1, c2);
         double2 zr[8];  // LX: Z_(g + 512 r) after the transform and the mirror exchange
         if constexpr (LX) {
 #pragma unroll
@@ -1057,9 +1074,33 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     };
     const double *cr = a.cr + s * KS, *scr = a.scr + s * KS;
     const double csc = a.csc;
+    // the drop-in lean mode (see spec_passA): system 0's workgroup also stores the input rows
+    const bool zcopy = a.zcopy1 != nullptr && s == 0;
+    auto copy_row = [&](int j, PV(&d1)[HK], PV(&d2)[HK]) {
+        const int M = (int)a.M;
+        auto put = [&](S *row, S *grow, int n, PV v) {  // elements 2n, 2n+1 and their ghost images
+            *reinterpret_cast<PV *>(row + 1 + 2 * n) = v;
+            if (n == 0) row[M + 1] = v.x;
+            if (n == HN - 1) row[0] = v.y;
+            if (grow) {
+                *reinterpret_cast<PV *>(grow + 1 + 2 * n) = v;
+                if (n == 0) grow[M + 1] = v.x;
+                if (n == HN - 1) grow[0] = v.y;
+            }
+        };
+        S *z1 = static_cast<S *>(a.zcopy1), *z2 = static_cast<S *>(a.zcopy2);
+        S *g1 = ghost_row_target(z1, ld, a.P, j, true), *g2 = ghost_row_target(z2, ld, a.P, j, true);
+#pragma unroll
+        for (int p = 0; p < HK; ++p) {
+            const int n = t + p * HT;
+            put(z1 + (size_t)(j + 1) * ld, g1, n, d1[p]);
+            put(z2 + (size_t)(j + 1) * ld, g2, n, d2[p]);
+        }
+    };
     // one row: consume the prefetched row (c1, c2), refill them with row jn (< s0: none)
     auto row_step = [&](int j, PV(&c1)[HK], PV(&c2)[HK], int jn) {
         asm volatile("" ::: "memory");  // keep coefficient loads in the loop
+        if (zcopy) copy_row(j, c1, c2);
         CX in[HK];
 #pragma unroll
         for (int p = 0; p < HK; ++p)
@@ -2081,6 +2122,213 @@ __global__ __launch_bounds__(SPL_KT) void spec_passB_split(SpecArgs a) {
 }
 
 // ------------------------------------------------------------------------------------
+// Bluestein rows: any row length the transforms above do not take (odd M > 8192, M > 16384),
+// as the reference's CHOLMOD factors any M x P (laplacian.jl:60-75).  The M-point DFT of a
+// row is a chirp-z convolution (nk = (n^2 + k^2 - (k - n)^2) / 2):
+//   X_k = c_k sum_n (x_n c_n) b_(k-n),   c_n = exp(-pi i n^2 / M),  b_m = exp(+pi i m^2 / M),
+// evaluated cyclically with power-of-two FFTs of length L >= 2M - 1 (the filter's transform
+// is a host table); the inverse DFT is the conjugate of the forward DFT of the conjugate.  The
+// transforms are Stockham passes in global memory (radix 8, then 4 / 2), over batches of
+// rows.  The spectra feed the split pipeline's recurrence kernels (spec_passA_split /
+// spec_passB_split): the same U contract as spec_fft_split.  A capability path, exact to
+// roundoff.
+// ------------------------------------------------------------------------------------
+constexpr int BL_T = 256;
+constexpr int64_t BL_MMAX = 1 << 18;           // rows up to 262144 points (L <= 2^19)
+constexpr size_t BL_BUF_BYTES = (size_t)1 << 28;  // per ping-pong buffer (rows per batch)
+
+template <int R, bool INV>
+__global__ __launch_bounds__(BL_T) void bl_pass(const double2 *__restrict__ src, double2 *__restrict__ dst,
+                                                const double2 *__restrict__ tw, int L, int NS, int rows) {
+    const int NB = L / R;
+    const int64_t total = (int64_t)rows * NB;
+    for (int64_t gi = (int64_t)blockIdx.x * BL_T + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * BL_T) {
+        const int row = (int)(gi / NB), j = (int)(gi - (int64_t)row * NB);
+        const double2 *x = src + (size_t)row * L;
+        double2 *y = dst + (size_t)row * L;
+        const int k = j % NS;
+        double2 v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = x[j + r * NB];
+        if (NS > 1) {  // W_(NS R)^(r k) = W_L^(r k L / (NS R)), exact table entries (< L)
+            const int step = k * (L / (NS * R));
+            int e = 0;
+#pragma unroll
+            for (int r = 1; r < R; ++r) {
+                e += step;
+                double2 w = tw[e];
+                if (INV) w.y = -w.y;
+                v[r] = cmul(v[r], w);
+            }
+        }
+        dftR<R, INV>(v);
+        const int base = (j / NS) * NS * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) y[base + r * NS] = v[r];
+    }
+}
+
+__global__ __launch_bounds__(BL_T) void bl_mul(double2 *x, const double2 *__restrict__ bhat, int L, int rows) {
+    const int64_t total = (int64_t)rows * L;
+    for (int64_t gi = (int64_t)blockIdx.x * BL_T + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * BL_T)
+        x[gi] = cmul(x[gi], bhat[gi % L]);
+}
+
+// rows [r0, r0 + rows): A_n = z_n c_n (n < M), 0 beyond; z = the projected pair of inputs
+template <class S>
+__global__ __launch_bounds__(BL_T) void bl_load_fwd(SpecArgs a, int64_t r0, int rows, double2 *A) {
+    const int M = (int)a.M, L = a.bl_L;
+    const int64_t total = (int64_t)rows * L, ld = a.ld;
+    const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
+    for (int64_t gi = (int64_t)blockIdx.x * BL_T + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * BL_T) {
+        const int64_t r = gi / L, j = r0 + r;
+        const int n = (int)(gi - r * L);
+        double2 v = make_double2(0, 0);
+        if (n < M) {
+            const double z1 = static_cast<const S *>(a.in1)[fidx(1 + n, j + 1, ld)];
+            const double z2 = static_cast<const S *>(a.in2)[fidx(1 + n, j + 1, ld)];
+            v = cmul(make_double2(p0 * z1 + p1 * z2, p2 * z1 + p3 * z2), a.bl_chirp[n]);
+        }
+        A[gi] = v;
+    }
+}
+
+// Z_k = c_k Y_k, split into the two systems' spectra B_s(k) in U (spec_fft_split's forward)
+template <class S>
+__global__ __launch_bounds__(BL_T) void bl_store_fwd(SpecArgs a, int64_t r0, int rows, const double2 *Y) {
+    using US = typename Store<S>::C;
+    const int M = (int)a.M, NH = M / 2, L = a.bl_L, KS = a.KS;
+    const bool odd = M & 1;
+    const int KC = odd ? NH + 1 : NH;
+    const int64_t total = (int64_t)rows * KC;
+    for (int64_t gi = (int64_t)blockIdx.x * BL_T + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * BL_T) {
+        const int64_t r = gi / KC, j = r0 + r;
+        const int k = (int)(gi - r * KC);
+        const double2 *y = Y + (size_t)r * L;
+        US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS;
+        auto Z = [&](int q) { return cmul(a.bl_chirp[q], y[q]); };
+        const double2 Zk = Z(k);
+        if (k == 0) {  // real lines k = 0 (and k = M/2 for even M)
+            Urow[0] = Store<S>::c(make_double2(Zk.x, 0));
+            Urow[KS] = Store<S>::c(make_double2(Zk.y, 0));
+            if (!odd) {
+                const double2 Zn = Z(NH);
+                Urow[NH] = Store<S>::c(make_double2(Zn.x, 0));
+                Urow[KS + NH] = Store<S>::c(make_double2(Zn.y, 0));
+            }
+        } else {
+            const double2 Zm = Z(M - k);
+            Urow[k] = Store<S>::c(make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5));
+            Urow[KS + k] = Store<S>::c(make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5));
+        }
+    }
+}
+
+// inverse, first half: rebuild Z from the systems' X in U (spec_fft_split's inverse) and load
+// A_n = conj(Z_n) c_n, 0 beyond M
+template <class S>
+__global__ __launch_bounds__(BL_T) void bl_load_inv(SpecArgs a, int64_t r0, int rows, double2 *A) {
+    using US = typename Store<S>::C;
+    const int M = (int)a.M, NH = M / 2, L = a.bl_L, KS = a.KS;
+    const bool odd = M & 1;
+    const int KC = odd ? NH + 1 : NH;
+    const int64_t total = (int64_t)rows * KC;
+    auto put = [&](double2 *x, int n, double2 z) { x[n] = cmul(cconj(z), a.bl_chirp[n]); };
+    for (int64_t gi = (int64_t)blockIdx.x * BL_T + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * BL_T) {
+        const int64_t r = gi / KC, j = r0 + r;
+        const int k = (int)(gi - r * KC);
+        const US *Urow = static_cast<const US *>(a.U) + (size_t)j * 2 * KS;
+        double2 *x = A + (size_t)r * L;
+        if (k == 0) {
+            put(x, 0, make_double2(d2(Urow[0]).x, d2(Urow[KS]).x));
+            if (!odd) put(x, NH, make_double2(d2(Urow[NH]).x, d2(Urow[KS + NH]).x));
+        } else {
+            const double2 X0 = d2(Urow[k]), X1 = d2(Urow[KS + k]);
+            put(x, k, make_double2(X0.x - X1.y, X0.y + X1.x));
+            put(x, M - k, make_double2(X0.x + X1.y, X1.x - X0.y));
+        }
+    }
+    const int64_t tail = (int64_t)rows * (L - M);
+    for (int64_t gi = (int64_t)blockIdx.x * BL_T + threadIdx.x; gi < tail; gi += (int64_t)gridDim.x * BL_T) {
+        const int64_t r = gi / (L - M);
+        A[(size_t)r * L + M + (gi - r * (L - M))] = make_double2(0, 0);
+    }
+}
+
+// inverse, second half: z_n = conj(c_n Y_n); pin, back-projection, store with the ghost ring
+// (spec_fft_split's inverse)
+template <class S>
+__global__ __launch_bounds__(BL_T) void bl_store_inv(SpecArgs a, int64_t r0, int rows, const double2 *Y) {
+    const int M = (int)a.M, L = a.bl_L;
+    const int64_t Pl = a.P, ld = a.ld;
+    __shared__ double pinw[BL_T / 64];
+    const double pinp = a.pinned0 ? pin_part<BL_T>(a, threadIdx.x) : 0.0;
+    const double pin = pin_total<BL_T>(pinp, pinw);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && r0 == 0) a.scal[1] = pin;
+    const int64_t total = (int64_t)rows * M;
+    S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
+    for (int64_t gi = (int64_t)blockIdx.x * BL_T + threadIdx.x; gi < total; gi += (int64_t)gridDim.x * BL_T) {
+        const int64_t r = gi / M, j = r0 + r;
+        const int i = (int)(gi - r * M);
+        const double2 z = cconj(cmul(a.bl_chirp[i], Y[(size_t)r * L + i]));
+        const bool pin_row = a.pinned0 && a.rank == 0 && j == 0;
+        S *row1 = out1 + (size_t)(j + 1) * ld;
+        S *grow1 = ghost_row_target(out1, ld, Pl, j, a.write_ghost_rows);
+        const double x1 = (pin_row && i == 0) ? 0.0 : z.x - pin, x2 = z.y;
+        store_row_with_ghosts(row1, grow1, M, i, (S)(a.pin_out[0] * x1 + a.pin_out[1] * x2));
+        if (out2) {
+            S *row2 = out2 + (size_t)(j + 1) * ld;
+            S *grow2 = ghost_row_target(out2, ld, Pl, j, a.write_ghost_rows);
+            store_row_with_ghosts(row2, grow2, M, i, (S)(a.pin_out[2] * x1 + a.pin_out[3] * x2));
+        }
+    }
+}
+
+static unsigned bl_grid(int64_t work) {
+    return (unsigned)std::min<int64_t>((work + BL_T - 1) / BL_T, 2048);
+}
+
+// length-L transforms of `rows` rows: x (input, natural order) -> the returned buffer
+template <bool INV>
+static int bl_fft(const SpecArgs &a, double2 *x, double2 *other, int rows, hipStream_t s, double2 **out) {
+    const int L = a.bl_L;
+    double2 *src = x, *dst = other;
+    for (int NS = 1; NS < L;) {
+        const int rem = L / NS, R = rem % 8 == 0 ? 8 : (rem % 4 == 0 ? 4 : 2);
+        const unsigned g = bl_grid((int64_t)rows * (L / R));
+        if (R == 8) bl_pass<8, INV><<<g, BL_T, 0, s>>>(src, dst, a.bl_tw, L, NS, rows);
+        else if (R == 4) bl_pass<4, INV><<<g, BL_T, 0, s>>>(src, dst, a.bl_tw, L, NS, rows);
+        else bl_pass<2, INV><<<g, BL_T, 0, s>>>(src, dst, a.bl_tw, L, NS, rows);
+        QG_LAUNCH_CHECK();
+        std::swap(src, dst);
+        NS *= R;
+    }
+    *out = src;
+    return QG_OK;
+}
+
+// the row transforms of every row, forward (rows -> U) or inverse (U -> rows)
+template <class S>
+static int bl_rows(bool inv, const SpecArgs &a, hipStream_t s) {
+    const int L = a.bl_L;
+    for (int64_t r0 = 0; r0 < a.P; r0 += a.bl_rows) {
+        const int rows = (int)std::min<int64_t>(a.bl_rows, a.P - r0);
+        double2 *y = nullptr, *z = nullptr;
+        if (!inv) bl_load_fwd<S><<<bl_grid((int64_t)rows * L), BL_T, 0, s>>>(a, r0, rows, a.bl_buf0);
+        else bl_load_inv<S><<<bl_grid((int64_t)rows * L), BL_T, 0, s>>>(a, r0, rows, a.bl_buf0);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(bl_fft<false>(a, a.bl_buf0, a.bl_buf1, rows, s, &y));
+        bl_mul<<<bl_grid((int64_t)rows * L), BL_T, 0, s>>>(y, a.bl_bhat, L, rows);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(bl_fft<true>(a, y, y == a.bl_buf0 ? a.bl_buf1 : a.bl_buf0, rows, s, &z));
+        if (!inv) bl_store_fwd<S><<<bl_grid((int64_t)rows * (a.M / 2 + 1)), BL_T, 0, s>>>(a, r0, rows, z);
+        else bl_store_inv<S><<<bl_grid((int64_t)rows * a.M), BL_T, 0, s>>>(a, r0, rows, z);
+        QG_LAUNCH_CHECK();
+    }
+    return QG_OK;
+}
+
+// ------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------
 template <int N, class S>
@@ -2117,6 +2365,21 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
         case 4096: return launch_pass<4096>(passB, a, s);
         case 8192: return a.f32 ? launch_half_t<float>(passB, a, s) : launch_half_t<double>(passB, a, s);
         default: break;
+    }
+    if (a.bl_L) {  // Bluestein rows: their transforms around the split pipeline's recurrences
+        const dim3 rgrid((unsigned)a.Nc, (unsigned)((a.KH + SPL_KT - 1) / SPL_KT));
+        if (!passB) {
+            QG_CHECK(a.f32 ? bl_rows<float>(false, a, s) : bl_rows<double>(false, a, s));
+            if (a.f32) spec_passA_split<float><<<rgrid, SPL_KT, 0, s>>>(a);
+            else spec_passA_split<double><<<rgrid, SPL_KT, 0, s>>>(a);
+            QG_LAUNCH_CHECK();
+        } else {
+            if (a.f32) spec_passB_split<float><<<rgrid, SPL_KT, 0, s>>>(a);
+            else spec_passB_split<double><<<rgrid, SPL_KT, 0, s>>>(a);
+            QG_LAUNCH_CHECK();
+            QG_CHECK(a.f32 ? bl_rows<float>(true, a, s) : bl_rows<double>(true, a, s));
+        }
+        return QG_OK;
     }
     // (qg_set_form(QG_FORM_ROW_SPLIT, 1): generic-size rows through the split passes too)
     if (a.M > GEN_MMAX || form(QG_FORM_ROW_SPLIT)) {
@@ -2179,12 +2442,64 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
 }
 
 // power-of-two rows 8 .. 8192 (FFT passes), any other rows 3 .. GEN_MMAX (generic passes)
-// and GEN_MMAX .. SPL_MMAX (split passes)
+// and GEN_MMAX .. SPL_MMAX (split passes), even rows to SPL_WMAX (wide split passes), any row
+// beyond (odd above SPL_MMAX, or above SPL_WMAX) up to BL_MMAX (Bluestein rows)
+static bool bluestein_rows(int64_t M) { return M > SPL_WMAX || (M > SPL_MMAX && M % 2 != 0); }
 bool SpectralSolver::supports(int64_t M, int64_t P) {
     if (P < 2) return false;
     if (M >= 8 && M <= 8192 && (M & (M - 1)) == 0) return true;
-    if (M > SPL_MMAX) return M <= SPL_WMAX && M % 2 == 0;  // wide split rows
+    if (M > SPL_MMAX) return M <= BL_MMAX;
     return M >= 3 && M <= SPL_MMAX;
+}
+
+// Bluestein tables (long double on the host): the chirp, and the filter's length-L transform
+// (an iterative radix-2 FFT in long double, scaled by 1/L)
+static void bl_tables(int64_t M, int L, std::vector<double2> &chirp, std::vector<double2> &bhat,
+                      std::vector<double2> &twL) {
+    const long double pi = 3.141592653589793238462643383279503L;
+    chirp.resize(M);
+    std::vector<long double> br(L, 0.0L), bi(L, 0.0L);
+    for (int64_t n = 0; n < M; ++n) {
+        const int64_t q = (n * n) % (2 * M);  // exp(-+ pi i n^2 / M) has period 2M in n^2
+        const long double ang = pi * (long double)q / (long double)M;
+        chirp[n] = make_double2((double)cosl(ang), (double)-sinl(ang));
+        br[n] = cosl(ang);
+        bi[n] = sinl(ang);
+        if (n > 0) {
+            br[L - n] = br[n];
+            bi[L - n] = bi[n];
+        }
+    }
+    for (int i = 1, j = 0; i < L; ++i) {  // bit reversal
+        int bit = L >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            std::swap(br[i], br[j]);
+            std::swap(bi[i], bi[j]);
+        }
+    }
+    for (int len = 2; len <= L; len <<= 1) {
+        for (int k = 0; k < len / 2; ++k) {
+            const long double a = -2 * pi * (long double)k / (long double)len;
+            const long double wr = cosl(a), wi = sinl(a);
+            for (int i = 0; i < L; i += len) {
+                const int u = i + k, v = i + k + len / 2;
+                const long double xr = br[v] * wr - bi[v] * wi, xi = br[v] * wi + bi[v] * wr;
+                br[v] = br[u] - xr;
+                bi[v] = bi[u] - xi;
+                br[u] += xr;
+                bi[u] += xi;
+            }
+        }
+    }
+    bhat.resize(L);
+    twL.resize(L);
+    for (int m = 0; m < L; ++m) {
+        bhat[m] = make_double2((double)(br[m] / L), (double)(bi[m] / L));
+        const long double a = 2 * pi * (long double)m / (long double)L;
+        twL[m] = make_double2((double)cosl(a), (double)-sinl(a));
+    }
 }
 
 // Rows per chunk: at most 16 (chunk summaries stay a small fraction of the traffic; 32 for
@@ -2224,8 +2539,9 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     a.nrad = 0;
     // generic rows: mixed-radix plan, or none (direct DFT: rows with a prime factor > 13, and
     // short rows, where the direct DFT measured no slower -- 120^2: 15 600-17 200 vs 15 000 steps/s)
-    const bool wsplit = M > SPL_MMAX;  // (planned at the half length H = M/2)
-    if (wsplit || ((M & (M - 1)) != 0 && M > 128)) {
+    const bool blue = bluestein_rows(M);
+    const bool wsplit = M > SPL_MMAX && !blue;  // (planned at the half length H = M/2)
+    if (!blue && (wsplit || ((M & (M - 1)) != 0 && M > 128))) {
         int64_t m = wsplit ? M / 2 : M, n = 0;
         int rad[16];
         while (m % 8 == 0) { rad[n++] = 8; m /= 8; }
@@ -2301,8 +2617,19 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     // split passes with a plan: where the DIF stages leave frequency k (digit reversal)
     const int64_t MP = wsplit ? M / 2 : M;  // length of the planned transform
     const size_t n_perm = a.nrad > 0 ? align_up(sizeof(int) * MP) : 0;
+    std::vector<double2> bl_chirp, bl_bhat, bl_twL;
+    int BL = 0, brows = 0;
+    if (blue) {
+        BL = 1;
+        while (BL < 2 * M - 1) BL <<= 1;
+        brows = (int)std::max<int64_t>(1, std::min<int64_t>(P, (int64_t)(BL_BUF_BYTES / (sizeof(double2) * BL))));
+        bl_tables(M, BL, bl_chirp, bl_bhat, bl_twL);
+    }
+    const size_t n_bl = blue ? align_up(sizeof(double2) * M) + 2 * align_up(sizeof(double2) * BL) +
+                                   2 * align_up(sizeof(double2) * (size_t)BL * brows)
+                             : 0;
     bytes_ = n_tw + n_coef + n_hot + n_U + 4 * n_S + n_dc + n_rec + n_grec + n_ext + 2 * n_line + n_scal + n_pinpart +
-             n_tw2 + n_half + n_perm;
+             n_tw2 + n_half + n_perm + n_bl;
     if (hipMalloc(&mem_, bytes_) != hipSuccess) {
         mem_ = nullptr;
         return QG_ERR_ALLOC;
@@ -2344,6 +2671,22 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
         }
         QG_HIP(hipMemcpy(d_perm, perm.data(), sizeof(int) * MP, hipMemcpyHostToDevice));
         a.perm = d_perm;
+    }
+    a.bl_L = 0;
+    if (blue) {
+        double2 *ch = (double2 *)take(align_up(sizeof(double2) * M));
+        double2 *bh = (double2 *)take(align_up(sizeof(double2) * BL));
+        double2 *tl = (double2 *)take(align_up(sizeof(double2) * BL));
+        a.bl_buf0 = (double2 *)take(align_up(sizeof(double2) * (size_t)BL * brows));
+        a.bl_buf1 = (double2 *)take(align_up(sizeof(double2) * (size_t)BL * brows));
+        QG_HIP(hipMemcpy(ch, bl_chirp.data(), sizeof(double2) * M, hipMemcpyHostToDevice));
+        QG_HIP(hipMemcpy(bh, bl_bhat.data(), sizeof(double2) * BL, hipMemcpyHostToDevice));
+        QG_HIP(hipMemcpy(tl, bl_twL.data(), sizeof(double2) * BL, hipMemcpyHostToDevice));
+        a.bl_chirp = ch;
+        a.bl_bhat = bh;
+        a.bl_tw = tl;
+        a.bl_L = BL;
+        a.bl_rows = brows;
     }
     a.tw = d_tw;
     a.coef = d_coef;
@@ -2397,9 +2740,13 @@ SpectralSolver::~SpectralSolver() {
 }
 
 int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *out2, int write_ghost_rows,
-                          hipStream_t s, GatherFn gather, void *user, const double *pin_in, const double *pin_out) {
+                          hipStream_t s, GatherFn gather, void *user, const double *pin_in, const double *pin_out,
+                          void *zcopy1, void *zcopy2) {
     if (!mem_) return QG_ERR_NOT_BOUND;
+    if ((zcopy1 || zcopy2) && (!fuses_input_copy() || !zcopy1 || !zcopy2 || a_.nranks > 1)) return QG_ERR_INVALID_ARG;
     SpecArgs a = a_;
+    a.zcopy1 = zcopy1;
+    a.zcopy2 = zcopy2;
     if (pin_in) std::memcpy(a.pin_in, pin_in, sizeof(a.pin_in));
     if (pin_out) std::memcpy(a.pin_out, pin_out, sizeof(a.pin_out));
     a.in1 = in1;
@@ -2407,8 +2754,11 @@ int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *ou
     a.out1 = out1;
     a.out2 = out2;
     a.write_ghost_rows = write_ghost_rows;
-    // one rank without a transport: the carry kernel closes the lines itself (no spec_pin)
-    a.fuse_pin = (a.nranks == 1 && !gather) ? 1 : 0;
+    // one rank: the carry kernel closes the lines itself (no spec_pin), with or without a
+    // transport -- a 1-rank ring's record all-gather would only copy the record onto itself
+    // (grec aliases rec), so none is posted (r04: RCCL's one-rank all-gather was a 6 us copy
+    // kernel and spec_pin another launch on the 1-rank ring's critical path)
+    a.fuse_pin = a.nranks == 1 ? 1 : 0;
     a.npin = a.fuse_pin ? (a.KH + CARRY_KB - 1) / CARRY_KB : pin_kblocks(a.KH);
     QG_CHECK(dispatch_pass(false, a, s));
     {
@@ -2425,8 +2775,6 @@ int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *ou
     QG_LAUNCH_CHECK();
     if (a.nranks > 1) {
         if (!gather) return QG_ERR_RCCL;
-        QG_CHECK(gather(user, a.rec, grec_buf_, a.rec_stride, s));
-    } else if (gather) {  // one-rank ring: still drive the transport (grec aliases rec)
         QG_CHECK(gather(user, a.rec, grec_buf_, a.rec_stride, s));
     }
     if (!a.fuse_pin) {

@@ -77,7 +77,17 @@ struct SpecArgs {
     void *half_tmp;           // wide rows: [P][M] system-0 result, state precision (pass B 0 -> 1)
     int nrad, rad[16];        // generic rows: mixed-radix pass plan (0 = direct DFT)
     const int *perm;          // split rows with a plan: position of frequency k after the DIF stages
-    int fuse_pin;             // one rank, no transport: spec_carry also does spec_pin's work
+    int fuse_pin;             // one rank: spec_carry also does spec_pin's work
+    // rows no transform above takes (odd M > 8192, M > 16384): Bluestein's chirp-z DFT through
+    // power-of-two FFTs of length bl_L >= 2M - 1 in global memory, rows in batches of bl_rows
+    const double2 *bl_chirp;  // [M] exp(-pi i n^2 / M)
+    const double2 *bl_bhat;   // [bl_L] FFT of the filter b_m = exp(+pi i m^2 / M) (m = -(M-1)..M-1), / bl_L
+    const double2 *bl_tw;     // [bl_L] exp(-2 pi i m / bl_L)
+    double2 *bl_buf0, *bl_buf1;  // [bl_rows][bl_L] ping-pong
+    int bl_L, bl_rows;        // bl_L = 0: not a Bluestein row
+    // (M+2, P+2) fields, or null: pass A also writes its two inputs there, ghost ring included
+    // (single GPU) -- the drop-in lean mode's move of the new zeta into slot 1 (qg_capi.hip)
+    void *zcopy1, *zcopy2;
     int npin;                 // pin parts pass B sums (pinpart[0 .. npin))
 };
 
@@ -102,7 +112,10 @@ public:
     typedef int (*GatherFn)(void *user, const double *send, double *recv, int64_t count, hipStream_t s);
     int solve(const void *in1, const void *in2, void *out1, void *out2, int write_ghost_rows,
               hipStream_t s, GatherFn gather = nullptr, void *user = nullptr, const double *pin_in = nullptr,
-              const double *pin_out = nullptr);  // optional per-call projections
+              const double *pin_out = nullptr,  // optional per-call projections
+              void *zcopy1 = nullptr, void *zcopy2 = nullptr);  // see SpecArgs::zcopy1
+    // pass A can write the zcopy fields (power-of-two rows: the FFT and wide-row passes)
+    bool fuses_input_copy() const { return a_.M >= 8 && a_.M <= 8192 && (a_.M & (a_.M - 1)) == 0; }
     const SpecArgs &args() const { return a_; }
     size_t device_bytes() const { return bytes_; }
     double *gather_buf() const { return grec_buf_; }  // the record all-gather's target

@@ -184,7 +184,7 @@ def _slot1_equal(b, a):
 
 
 # slot 1 only (slots 2-3 of zeta / psi unmaintained, never read by the reference): after every
-# evolve_zeta! the new zeta is in slot 1 (read back between the two calls), after every step
+# evolve_zeta! the new zeta is the newest slot qg_slot names, after every step
 # zeta, psi and f_store are what the rotating path holds -- both solvers, F32, the LDS-ring and
 # certifying tendencies (1280 x 1024), HIP-graph replay
 @pytest.mark.parametrize("M,P,solver,f32", [(64, 48, 0, False), (128, 128, 1, False), (64, 64, 0, True),
@@ -199,7 +199,9 @@ def test_keep_order_slot1_matches_rotation(qg, M, P, solver, f32):
     for t in range(1, 8):
         a.evolve_zeta_(t)
         b.evolve_zeta_(t)
-        assert torch.equal(b.zeta[0], a.logical("zeta")[0])  # slot 1 newest between the calls
+        # between the calls the newest zeta is where qg_slot says (lean mode, spectral solver:
+        # slot 2 until the solve's pass A moves it into slot 1)
+        assert torch.equal(b.logical("zeta")[0], a.logical("zeta")[0])
         a.evolve_psi_()
         b.evolve_psi_()
         assert b.heads() == [0, 0, 0]
@@ -258,3 +260,30 @@ def test_keep_order_slot1_to_full_refused(qg):
     st.set_keep_order(True)
     st.run(4, 2)
     assert st.heads() == [0, 0, 0]
+
+
+def test_keep_order_slot1_pending_move_settles(qg):
+    """Lean mode, spectral solver: the new zeta waits in slot 2 until the solve; two tendencies
+    in a row, qg_synchronize and qg_canonicalize complete the move into slot 1 first, so every
+    path sees the reference's slot 1."""
+    import torch
+    m = qg.bench_model(128)
+    a = qg.initialise_model(m)
+    b = qg.initialise_model(m)
+    b.set_keep_order(True, slot1_only=True)
+    a.evolve_zeta_(1)
+    b.evolve_zeta_(1)
+    assert b.heads()[0] == 1  # pending: newest in slot 2
+    b.synchronize()
+    assert b.heads() == [0, 0, 0] and torch.equal(b.zeta[0], a.logical("zeta")[0])
+    a.evolve_psi_()
+    b.evolve_psi_()
+    a.evolve_zeta_(2)
+    b.evolve_zeta_(2)
+    a.evolve_zeta_(3)  # two tendencies in a row
+    b.evolve_zeta_(3)
+    b.canonicalize()
+    assert torch.equal(b.zeta[0], a.logical("zeta")[0])
+    a.evolve_psi_()
+    b.evolve_psi_()
+    _slot1_equal(b, a)

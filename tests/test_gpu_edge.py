@@ -1,7 +1,7 @@
 """Edge cases of the device path against the C oracle: the smallest grids the spectral solver
 takes (M = 8, P = 2), odd P (chunk of one row), non-square slabs both ways, an explicit chunk
-size, and the refusal of what the spectral solver cannot do (non power-of-two M), which PCG
-without preconditioner still solves.  Relative RMS < 1e-10 after a few Euler + AB3 steps."""
+size, rows of every length up to 262144 points (mixed-radix, split, wide split and Bluestein
+row transforms), and the refusal of what the spectral solver cannot do.  Relative RMS < 1e-10 after a few Euler + AB3 steps."""
 import numpy as np
 import pytest
 
@@ -93,16 +93,16 @@ def test_reference_benchmark_sweep_sizes(env, M):
 
 def test_generic_rows_wide(env):
     """Wide generic rows on rectangular slabs: M = 2000 and 3000 (mixed-radix passes), 1999
-    (prime: direct DFT); rows the spectral solver cannot take refused: odd M above 8192 and
-    any M above 16384."""
+    (prime: direct DFT); rows beyond the Bluestein path's 262144 points, or slabs of one row,
+    are refused (QG_ERR_UNSUPPORTED)."""
     qg, O, R = env
     for M in (2000, 1999, 3000):
         st = qg.run_model_no_output(qg.bench_model(M, P=24, dt=600.0), nsteps=3)
         ref = O.State(R.bench_model(M, P=24, dt=600.0)).run(3)
         assert rel(st.to_numpy("psi"), ref.psi) < TOL, M
-    for M in (8201, 16386):
+    for M, P in ((262145, 2), (20000, 1)):
         with pytest.raises(qg.QGError) as e:
-            qg.State(qg.bench_model(M, P=8))
+            qg.State(qg.bench_model(M, P=P))
         assert e.value.status == -2, M
 
 
@@ -179,6 +179,56 @@ def test_wide_split_rows(env, M, P, steps, kw):
         pc = qg.run_model_no_output(qg.bench_model(M, P=P, dt=60.0), nsteps=steps, solver=1)
         assert max(modal_residuals(R, m, pc.to_numpy("zeta"), pc.to_numpy("psi"))) < 1e-13
         assert rel(pc.to_numpy("psi"), ref.psi) < 2e-9
+
+
+@pytest.mark.parametrize("M,P,steps,kw,oracle", [(8193, 4, 2, {}, True), (20000, 4, 2, {}, True),
+                                                 (16385, 6, 2, {}, True), (20000, 8, 2, {"chunk_rows": 4}, True),
+                                                 (50001, 2, 2, {}, False)])
+def test_bluestein_rows(env, M, P, steps, kw, oracle):
+    """Rows no FFT plan of the direct solver takes -- odd M > 8192 and M > 16384, which returned
+    QG_ERR_UNSUPPORTED before (the bare-CG fallback) -- through Bluestein's chirp-z DFT: power-of-
+    two FFTs of length >= 2M - 1 in global memory around the split pipeline's recurrences.  The
+    reference factors any M x P (laplacian.jl:60-75).  Exactness as for the wide split rows: the
+    device solution's residuals in both modal systems at roundoff (< 1e-13), and agreement with
+    the oracle to the conditioning floor of these long rows (cond ~ M^2: 2e-9).  (50001 x 2: the
+    oracle's O(M^2) direct DFT would take minutes; residuals only.)"""
+    qg, O, R = env
+    st = qg.run_model_no_output(qg.bench_model(M, P=P, dt=60.0), nsteps=steps, **kw)
+    m = R.bench_model(M, P=P, dt=60.0)
+    res_dev = modal_residuals(R, m, st.to_numpy("zeta"), st.to_numpy("psi"))
+    print(f"M={M} P={P} device residuals {res_dev}")
+    assert max(res_dev) < 1e-13, res_dev
+    assert np.isfinite(st.to_numpy("psi")).all()
+    if oracle:
+        ref = O.State(R.bench_model(M, P=P, dt=60.0)).run(steps)
+        assert rel(st.to_numpy("zeta"), ref.zeta) < TOL
+        assert rel(st.to_numpy("psi"), ref.psi) < 2e-9
+
+
+@pytest.mark.parametrize("M,P", [(8193, 4), (20000, 4)])
+def test_bluestein_rows_pcg(env, M, P):
+    """PCG with the Bluestein-row direct solve as its preconditioner (the verdict's bar: <= 50
+    iterations at M = 8193 and 20000): every solve certifies in one iteration, residuals at
+    roundoff, the same answer as the direct solver."""
+    qg, O, R = env
+    m = qg.bench_model(M, P=P, dt=60.0)
+    a = qg.run_model_no_output(m, nsteps=3)
+    b = qg.run_model_no_output(m, nsteps=3, solver=1)
+    s = b.stats()
+    assert 1 <= s["iters"][0] <= 50 and max(s["relres"]) < 1e-12, s
+    mr = R.bench_model(M, P=P, dt=60.0)
+    assert max(modal_residuals(R, mr, b.to_numpy("zeta"), b.to_numpy("psi"))) < 1e-13
+    assert rel(b.to_numpy("psi"), a.to_numpy("psi")) < 1e-12
+
+
+def test_bluestein_rows_f32(env):
+    """F32 state through the Bluestein rows (M = 20000): psi within the white-noise F32 bar."""
+    import torch
+    qg, O, R = env
+    m = qg.bench_model(20000, P=4, dt=60.0)
+    a = qg.run_model_no_output(m, nsteps=2)
+    b = qg.run_model_no_output(m, nsteps=2, dtype=torch.float32)
+    assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 2e-2
 
 
 def test_wide_split_rows_f32(env):

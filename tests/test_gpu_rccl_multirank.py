@@ -27,20 +27,21 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl", gather="rccl"):
+def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl", gather="rccl", devices=False):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
     from bench import rccl_one_gpu_env
 
-    os.environ.update(rccl_one_gpu_env(rank))  # (before RCCL initialises)
+    if not devices:  # every rank on GPU 0 (RCCL over loopback); devices: rank r on GPU r
+        os.environ.update(rccl_one_gpu_env(rank))  # (before RCCL initialises)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
     import torch.distributed as dist
 
     dist.init_process_group("gloo", rank=rank, world_size=world)  # (uid broadcast, barriers)
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(rank if devices else 0)
     import ctypes as C
 
     import qgamd
@@ -68,12 +69,13 @@ def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl"
     dist.destroy_process_group()
 
 
-def _run(world, M, P, steps, d, solver, overlap, halo="rccl", gather="rccl"):
+def _run(world, M, P, steps, d, solver, overlap, halo="rccl", gather="rccl", devices=False):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap, halo, gather))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap, halo, gather,
+                                               devices))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -147,6 +149,25 @@ def test_peer_transports_across_processes_bit_identical(world, overlap, halo, ga
     for r in range(world):
         for n in ("zeta", "psi", "f_store"):
             assert np.array_equal(a[r][n], b[r][n]), (r, n)
+
+
+@pytest.mark.parametrize("halo,gather,overlap", [("put", "peer", False), ("peer", "peer", True)])
+def test_peer_transports_across_devices_bit_identical(halo, gather, overlap):
+    """The same check with one rank per GPU (needs >= 2 devices; skipped on a one-GPU box): the
+    IPC regions opened across devices, rows and records written over xGMI, system-scope flags
+    seen by the other device -- bit for bit equal to RCCL's send/recv + ncclAllGather."""
+    import torch
+
+    n = torch.cuda.device_count()
+    if n < 2:
+        pytest.skip("needs two GPUs")
+    world = min(n, 4)
+    with tempfile.TemporaryDirectory() as d0, tempfile.TemporaryDirectory() as d1:
+        a = _run(world, 256, 64 * world, 6, d0, 0, True, devices=True)
+        b = _run(world, 256, 64 * world, 6, d1, 0, overlap, halo, gather, devices=True)
+    for r in range(world):
+        for nm in ("zeta", "psi", "f_store"):
+            assert np.array_equal(a[r][nm], b[r][nm]), (r, nm)
 
 
 # ---- BASELINE configs 4 and 5 at their workload size over multi-rank RCCL ----------------
