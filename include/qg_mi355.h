@@ -67,7 +67,9 @@ typedef enum {
     QG_SOLVER_SPECTRAL = 0, /* direct: x-DFT + parallel cyclic tridiagonal solve in y;    *
                              * any M in 3..262144 (M = 2^k <= 8192: FFT passes; odd M     *
                              * above 8192 and M above 16384: Bluestein row transforms),   *
-                             * P >= 2, else UNSUPPORTED                                   */
+                             * P >= 2 per rank, else UNSUPPORTED.  Both solvers refuse   *
+                             * a global P (or M) of 2: the reference's matrix is not the  *
+                             * periodic 5-point operator there (laplacian.jl:41-46)       */
     QG_SOLVER_PCG = 1       /* matrix-free PCG on the 5-point operator                     */
 } qg_solver_kind;
 

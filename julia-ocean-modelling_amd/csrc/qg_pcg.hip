@@ -429,6 +429,9 @@ int PcgSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nranks,
                     int pinned0, const double proj_in[4], const double proj_out[4], int precond, double rtol,
                     int maxit, int chunk_rows) {
     if (M < 2 || P < 2 || !(dx > 0) || nranks < 1 || P_total != P * nranks) return QG_ERR_INVALID_ARG;
+    // two points in a periodic direction: the reference's matrix is not the periodic 5-point
+    // operator there (laplacian.jl:41-46 overwrites the wrap entry), see SpectralSolver::init
+    if (M < 3 || P_total < 3) return QG_ERR_UNSUPPORTED;
     PcgArgs &a = a_;
     a.M = M;
     a.P = P;

@@ -118,6 +118,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
             om[q][s] = make_double2(1, 1);
         }
     const double p0 = a.pin_in[0], p1 = a.pin_in[1], p2 = a.pin_in[2], p3 = a.pin_in[3];
+    const double csch = 0.5 * a.csc;
     double dc = 0;
     double *hline = a.hline;
     // register prefetch: row j-1 is loaded while row j is transformed (the barriers only wait
@@ -250,14 +251,15 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                         om[q][s] = make_double2(om[q][s].x * r0, om[q][s].y * rN);
                     }
                 } else {
-                    const double2 B[2] = {make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5),
-                                          make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5)};
+                    // 2 B_s: the split's halves ride in the scale, r (csc / 2) = (r csc) / 2
+                    // exactly (a power of two), so u is bit for bit the halved form's
+                    const double2 B[2] = {make_double2(Zk.x + Zm.x, Zk.y - Zm.y), make_double2(Zk.y + Zm.y, Zm.x - Zk.x)};
 #pragma unroll
                     for (int s = 0; s < 2; ++s) {
                         const int o = s * KS + k;
                         const double r = QG_PA_R(q, s, o);  // cs = r csc
                         (void)o;
-                        u[q][s] = cfma(r, u[q][s], cscale(B[s], r * a.csc));
+                        u[q][s] = cfma(r, u[q][s], cscale(B[s], r * csch));
                         st_u(Urow + s * KS + (LX ? t + q * T : k), Store<S>::c(u[q][s]));
                         bw[q][s] = cfma(om[q][s].x, u[q][s], bw[q][s]);
                         om[q][s].x *= r;
@@ -1073,7 +1075,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         }
     };
     const double *cr = a.cr + s * KS, *scr = a.scr + s * KS;
-    const double csc = a.csc;
+    const double csc = a.csc, csch = 0.5 * csc;
     // the drop-in lean mode (see spec_passA): system 0's workgroup also stores the input rows
     const bool zcopy = a.zcopy1 != nullptr && s == 0;
     auto copy_row = [&](int j, PV(&d1)[HK], PV(&d2)[HK]) {
@@ -1097,9 +1099,18 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
             put(z2 + (size_t)(j + 1) * ld, g2, n, d2[p]);
         }
     };
+    // F32 states: r of this thread's lines loaded once -- row-invariant -- and held in
+    // registers instead of re-read from L2 every row, where each row's loads queue behind the
+    // next row's prefetch (vmcnt retires in order).  (F64 states: the 16 registers would spill.)
+    constexpr bool RQ_HOIST = std::is_same<S, float>::value;
+    double rq[HK];
+    if constexpr (RQ_HOIST) {
+#pragma unroll
+        for (int q = 0; q < HK; ++q) rq[q] = scr[t + q * HT];
+    }
     // one row: consume the prefetched row (c1, c2), refill them with row jn (< s0: none)
     auto row_step = [&](int j, PV(&c1)[HK], PV(&c2)[HK], int jn) {
-        asm volatile("" ::: "memory");  // keep coefficient loads in the loop
+        if constexpr (!RQ_HOIST) asm volatile("" ::: "memory");  // keep coefficient loads in the loop
         if (zcopy) copy_row(j, c1, c2);
         CX in[HK];
 #pragma unroll
@@ -1132,12 +1143,14 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 om[q] = make_double2(om[q].x * r0, om[q].y * rN);
             } else {
                 const double2 Zm = t == 0 ? in[(8 - q) & 7] : in[7 - q];  // Z_(HN - k)
-                // E = (Z_k + conj Z_{HN-k}) / 2, O = (Z_k - conj Z_{HN-k}) / 2i, X = E + W^k O
-                const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
-                const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
+                // E = (Z_k + conj Z_{HN-k}) / 2, O = (Z_k - conj Z_{HN-k}) / 2i, X = E + W^k O,
+                // formed as 2E, 2O, 2X: the halves ride in the scale r (csc / 2), a power of
+                // two, so u is bit for bit the halved form's
+                const double2 E = make_double2(Zk.x + Zm.x, Zk.y - Zm.y);
+                const double2 O = make_double2(Zk.y + Zm.y, Zm.x - Zk.x);
                 const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
-                const double r = scr[t + q * HT];
-                u[q] = cfma(r, u[q], cscale(X, r * csc));
+                const double r = RQ_HOIST ? rq[q] : scr[t + q * HT];
+                u[q] = cfma(r, u[q], cscale(X, r * csch));
                 st_u(Urow + t + q * HT, Store<S>::c(u[q]));
                 bw[q] = cfma(om[q].x, u[q], bw[q]);
                 om[q].x *= r;
@@ -2522,6 +2535,12 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
                          int chunk_rows, int f32) {
     if (!supports(M, P)) return QG_ERR_UNSUPPORTED;
     if (!(dx > 0) || nranks < 1 || rank < 0 || rank >= nranks || P_total != P * nranks) return QG_ERR_INVALID_ARG;
+    // two rows in all: the reference's laplacian_1d_periodic (laplacian.jl:41-46) writes its
+    // wrap entry over the neighbour entry (lap[1, end] = 1 where both neighbours of a row are
+    // the same row), so its matrix is not the periodic 5-point operator its tendency applies;
+    // refused rather than solving a different system (the C oracle, like this solver, would
+    // solve the periodic one: 0.28 relative residual against the reference's matrix)
+    if (P_total < 3) return QG_ERR_UNSUPPORTED;
     const int L = pick_chunk(M, P, chunk_rows);
     if (L < 1) return QG_ERR_INVALID_ARG;
     SpecArgs &a = a_;
