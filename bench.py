@@ -119,7 +119,69 @@ def parse():
                          "halo overlap toggled (overlap_ab)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
+    ap.add_argument("--no-pmc-live", dest="pmc_live", action="store_false", default=True,
+                    help="N = 1: skip measuring roofline.traffic live (two rocprofv3 --pmc child runs of "
+                         "this workload, FETCH_SIZE and WRITE_SIZE, ~20 s each); the committed "
+                         "profiles/pmc_tendency.json is used instead")
     return ap.parse_args()
+
+
+PMC_KERNEL = "tendency"  # substring of the dominant kernel's name (tendency_kernel / tendency_pair_kernel)
+
+
+def pmc_live(args, timeout_s=150):
+    """roofline.traffic of THIS run's workload: rocprofv3 --kernel-trace --pmc FETCH_SIZE, then
+    WRITE_SIZE (one counter per pass, never with other traces), each a child process running 5
+    steps of the same configuration; HBM bytes per launch of the dominant kernel with the
+    gfx950 corrections of the MI355X guide (KiB -> bytes; FETCH_SIZE x2, WRITE_SIZE x1), the
+    two Euler launches skipped.  Returns (bytes, note) or (None, reason)."""
+    import csv
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if rp is None:
+        return None, "rocprofv3 not found"
+    tmp = tempfile.mkdtemp(prefix="qg_pmc_", dir="/tmp")
+    env = dict(os.environ, TMPDIR="/tmp")
+    child = [sys.executable, os.path.abspath(__file__), "--n", str(args.n), "--dtype", args.dtype,
+             "--dt", str(args.dt), "--steps", "5", "--warmup", "3", "--clock-warm-ms", "0",
+             "--cpu-steps", "0", "--cpu-steps-1t", "0", "--pcg-steps", "0", "--dropin-steps", "0",
+             "--no-pmc-live"]
+    vals = {}
+    try:
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, ctr.lower())
+            cmd = [rp, "--kernel-trace", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p", "--"] + child
+            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=subprocess.DEVNULL,
+                                 stderr=subprocess.DEVNULL, start_new_session=True)
+            try:
+                rc = p.wait(timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return None, f"{ctr} pass timed out"
+            if rc != 0:
+                return None, f"{ctr} pass exited {rc}"
+            files = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith("counter_collection.csv")]
+            if not files:
+                return None, f"{ctr} pass wrote no counter file"
+            v = []
+            with open(files[0]) as f:
+                for row in csv.DictReader(f):
+                    if row.get("Counter_Name") == ctr and PMC_KERNEL in row.get("Kernel_Name", ""):
+                        v.append(float(row["Counter_Value"]))
+            v = v[2:] if len(v) > 2 else v  # (the two Euler launches move less)
+            if not v:
+                return None, f"{ctr}: no {PMC_KERNEL} dispatches"
+            vals[ctr] = (sum(v) / len(v) * 1024, len(v))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    rd, wr = 2 * vals["FETCH_SIZE"][0], vals["WRITE_SIZE"][0]
+    return rd + wr, (f"live: rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE per launch, child runs of this workload "
+                     f"({vals['FETCH_SIZE'][1]} / {vals['WRITE_SIZE'][1]} AB3 launches), read {rd / 1e9:.3f} GB "
+                     f"+ write {wr / 1e9:.3f} GB")
 
 
 def choose_transports(qgamd, st, halo, gather, spectral):
@@ -144,6 +206,39 @@ def choose_transports(qgamd, st, halo, gather, spectral):
     if "auto" in (halo, gather):
         return "auto: peer regions set up on every rank"
     return "as requested"
+
+
+def verify_peer(st, torch, dist, steps=3):
+    """The chosen peer transports against RCCL before they carry the headline (collective):
+    `steps` steps from the initial state with each, every slot of zeta and psi compared bit for
+    bit on every rank -- the two are bit-identical by construction
+    (tests/test_gpu_rccl_multirank.py), so a stale or torn exchange between devices shows as a
+    mismatch.  Leaves the peer transports set when they agree; else RCCL, and returns why."""
+    halo, gather = st.halo_transport, getattr(st, "gather_transport", "rccl")
+
+    def run_digest():
+        st.initialise()
+        st.run(1, steps)
+        torch.cuda.synchronize()
+        return [x.detach().clone() for x in (st.zeta, st.psi)]
+
+    a = run_digest()
+    st.set_halo_transport("rccl")
+    if gather != "rccl":
+        st.set_gather_transport("rccl")
+    b = run_digest()
+    iv = torch.int32 if a[0].dtype == torch.float32 else torch.int64
+    same = all(torch.equal(x.view(iv), y.view(iv)) for x, y in zip(a, b))
+    del a, b
+    flag = torch.tensor([0 if same else 1], dtype=torch.int32, device="cuda")
+    if dist is not None:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    if int(flag.item()):
+        return f"peer transports differed from RCCL after {steps} steps on some rank"
+    st.set_halo_transport(halo)
+    if gather != "rccl":
+        st.set_gather_transport(gather)
+    return None
 
 
 def _cpu_model():
@@ -421,6 +516,20 @@ def main():
     st.initialise()
     torch.cuda.synchronize()
     setup_ms = (time.perf_counter() - t_setup) * 1e3
+    transport_check = None
+    if transport_choice is not None and (cur_halo != "rccl" or cur_gather != "rccl"):
+        # (not part of setup_ms: a guard of this run, not of the library's set-up)
+        why = verify_peer(st, torch, dist)
+        if why is None:
+            transport_check = "peer transports == RCCL bit for bit over 3 steps on every rank"
+        else:
+            transport_check = why
+            transport_choice = f"rccl: {why}"
+            cur_halo, cur_gather = "rccl", "rccl"
+            overlap = args.overlap if args.overlap is not None else True
+            st.set_overlap(overlap)
+        st.initialise()
+        torch.cuda.synchronize()
 
     # the north star's PCG leg first: real work on the same grid that also brings the GPU
     # clock up before the measured model's warm-up (single GPU only)
@@ -620,14 +729,22 @@ def main():
     ms = el * 1e3 / K
     tend_gbs = BYTES_TENDENCY_AB3 * pts / (tend_ms * 1e-3) / 1e9
     step_gbs = BYTES_STEP * pts / (ms * 1e-3) / 1e9
-    traffic, pmc_tag = None, None
+    traffic, pmc_tag, traffic_source = None, None, None
+    if args.pmc_live and world == 1 and not args.comm_self and args.solver == "spectral":
+        traffic, note = pmc_live(args)
+        if traffic is not None:
+            traffic_source = note
+        else:
+            print(f"bench: live PMC traffic unavailable ({note}); using the committed file", file=sys.stderr)
     prof = os.path.join(ROOT, "profiles", "pmc_tendency.json")
-    if os.path.exists(prof):
+    if traffic is None and os.path.exists(prof):
         try:
             pj = json.load(open(prof))
             if pj.get("n") == n and args.dtype == "f64" and args.solver == "spectral":
                 traffic = pj.get("hbm_bytes_per_launch")
                 pmc_tag = pj.get("tag")
+                traffic_source = ("committed profiles/pmc_tendency.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE "
+                                  f"per launch, box {pmc_tag}")
         except Exception:
             traffic = None
     out = {
@@ -663,6 +780,7 @@ def main():
                           if world > 1 else ("rccl (1-rank ring)" if args.comm_self else "none")),
             "halo_overlap": bool(overlap and (world > 1 or args.comm_self)),
             "transport_choice": transport_choice,
+            "transport_check": transport_check,
             "halo_transport": (cur_halo if args.transport == "rccl" and (world > 1 or args.comm_self) else None),
             "gather_transport": (cur_gather if args.transport == "rccl" and (world > 1 or args.comm_self)
                                  and args.solver == "spectral" else None),
@@ -675,8 +793,7 @@ def main():
             "unit": "GB/s",
             "frac": tend_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "traffic_source": ("profiles/pmc_tendency.json: rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch, "
-                               f"box {pmc_tag}" if traffic is not None else None),
+            "traffic_source": traffic_source if traffic is not None else None,
             "avg_launch_ms": tend_ms,
             "algorithmic_bytes_per_launch": BYTES_TENDENCY_AB3 * pts,
         },

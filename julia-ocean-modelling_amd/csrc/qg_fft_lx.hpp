@@ -147,17 +147,48 @@ struct NoHook {
     __device__ void operator()() const {}
 };
 
+// Stage 2's twiddle base W^(64 c0) depends on the wave only (c0 = wave), so its powers w^1..w^7
+// can be formed once per kernel and held in scalar registers: the row loop then skips the six
+// complex multiplies per thread that form them (the same recurrence, so bit-identical values).
+struct Stage2Tw {
+    double2 p[7];
+};
+struct NoTw2 {};
+__device__ __forceinline__ double uniform_d(double x) {
+    return mkd((unsigned)__builtin_amdgcn_readfirstlane((int)lo32(x)),
+               (unsigned)__builtin_amdgcn_readfirstlane((int)hi32(x)));
+}
+template <bool INV>
+__device__ __forceinline__ Stage2Tw stage2_powers(const double2 *tw512, int t) {
+    double2 w = tw512[64 * (t >> 6)];
+    if (INV) w.y = -w.y;
+    Stage2Tw s;
+    double2 wr = w;
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+        s.p[r] = make_double2(uniform_d(wr.x), uniform_d(wr.y));
+        if (r < 6) wr = cmul(wr, w);
+    }
+    return s;
+}
+
 // The transform.  v: in: element g_in + 512 r (register r); out: element g_out + 512 r.
 // b0, b1: two LDS row buffers (N double2 each); tw512: the LDS twiddle table.  The caller
 // guarantees that no thread still reads b0 / b1 from an earlier use when it enters (two calls
 // in a row are safe: b0's reads end before T2's barrier, b1's before the next call's T1
 // barrier).  `hook` runs after T1's LDS writes, while v holds nothing live (the place for the
 // next row's prefetch loads: their registers are not live beside v's).
-template <bool INV, bool IN_MIRROR, bool OUT_MIRROR, class Hook = NoHook>
+// ONE_BUF: T2 reuses b0 (b1 is ignored): half the LDS (two workgroups per CU) for two more
+// barriers -- T2's writes wait for every wave's T1 reads, and T1's writes for the previous
+// call's T2 reads, so the caller needs no guarantee.
+// s2: stage 2's twiddle powers (stage2_powers<INV>), or NoTw2 to form them from tw512.
+template <bool INV, bool IN_MIRROR, bool OUT_MIRROR, bool ONE_BUF = false, class Hook = NoHook, class Tw2 = NoTw2>
 __device__ __forceinline__ void fft(double2 (&v)[8], double2 *b0, double2 *b1, const double2 *tw512, int t,
-                                    Hook &&hook = Hook()) {
+                                    Hook &&hook = Hook(), const Tw2 &s2 = Tw2()) {
     const int w = t >> 6, l = t & 63;
+    if constexpr (ONE_BUF) b1 = b0;
     dft8<INV>(v);  // stage 1 -> c0 in the register index
+    if constexpr (ONE_BUF) __syncthreads();
     {
         const int g = IN_MIRROR ? mirror_group(t) : t;
 #pragma unroll
@@ -167,9 +198,16 @@ __device__ __forceinline__ void fft(double2 (&v)[8], double2 *b0, double2 *b1, c
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 8; ++r) v[r] = b0[w * 512 + r * 64 + l];  // wave c0, register d2
-    stage<INV>(v, tw512[64 * w]);      // -> c1
+    if constexpr (std::is_same<Tw2, Stage2Tw>::value) {  // -> c1
+#pragma unroll
+        for (int r = 1; r < 8; ++r) v[r] = cmul(v[r], s2.p[r - 1]);
+        dft8<INV>(v);
+    } else {
+        stage<INV>(v, tw512[64 * w]);
+    }
     swap_regs_lanes345(v);             // register d1, lane bits 3-5 c1
     stage<INV>(v, tw512[8 * (w + 8 * (l >> 3))]);  // -> c2
+    if constexpr (ONE_BUF) __syncthreads();
     {
         const int d0 = l & 7, mb = w + 8 * (l >> 3);
 #pragma unroll

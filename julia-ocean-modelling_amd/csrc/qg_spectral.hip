@@ -168,6 +168,10 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
                 rqh[q][s] = (NH % T == 0 || k < NH) ? QG_CR(s * KS + k) : 0.0;
             }
     }
+    // LX: stage 2's twiddle powers in scalar registers (see lx::Stage2Tw; measured 106.1 ->
+    // 104.5 us at 4096^2, r05i)
+    lx::Stage2Tw s2f{};
+    if constexpr (LX) s2f = lx::stage2_powers<false>(a.tw, t);
     // one row: consume the prefetched row (c1, c2), refill them with row j - 1, transform,
     // split, filter
     auto row_step = [&](int j, auto &c1, auto &c2) {
@@ -194,7 +198,7 @@ __global__ __launch_bounds__(Geo<N>::T, Geo<N>::MINW) void spec_passA(SpecArgs a
             const int tt = opaque_tid();
             lx::fft<false, false, true>(zr, b0, b1, twl, tt, [&]() {
                 if (PF && j - 1 >= s0) load_into(j - 1, c1, c2);
-            });
+            }, s2f);
             lx::mirror_exchange(zr, stash, tt);
         } else if constexpr (Plan::REG_IN) {  // first FFT pass straight from the prefetch registers
             double2 in[Plan::R0];
@@ -983,26 +987,41 @@ constexpr int HT = 512;            // threads per workgroup
 constexpr int HK = HN / HT;        // wavenumber slots per thread (k_q above); slot (q 0, t 0)
                                    // packs the real lines k = 0 (.x) and k = HN (.y)
 static_assert(HN == lx::N && HT == lx::T && HK == 8, "wide-row transform geometry");
-// LDS: the transform's two row buffers, its twiddles and the mirror stash (lx::LDS_ELEMS),
-// then the two-level split-step twiddles (64 + 64).  (The transforms stay F64 for F32 states too: computing pass A's in F32 saved
+// LDS: the transform's two row buffers, its twiddles and the mirror stash (lx::LDS_ELEMS).
+// (The transforms stay F64 for F32 states too: computing pass A's in F32 saved
 // 18 of 392 us at 8192^2 and pass B's 16 of 417, while the F32 error grew -- psi 2.3e-3 ->
 // 5.3e-3 against the oracle at 8192 x 16, zeta 1e-4 -> 1e-3 on the smooth field with pass B's
 // in F32 (r04e; qg_fft.hpp keeps the complex type a template parameter).)
-constexpr size_t half_lds_bytes() { return sizeof(double2) * (lx::LDS_ELEMS + 128); }
+constexpr size_t half_lds_bytes() { return sizeof(double2) * lx::LDS_ELEMS; }
 struct HalfLds {
-    double2 *b0, *b1, *tw512, *stash, *wlo, *whi;
+    double2 *b0, *b1, *tw512, *stash;
     __device__ explicit HalfLds(void *base) {
         b0 = static_cast<double2 *>(base);
         b1 = b0 + HN;
         tw512 = b1 + HN;
         stash = tw512 + 512;
-        wlo = b0 + lx::LDS_ELEMS;
-        whi = wlo + 64;
     }
 };
 // line q of thread t (mirror group g, partner group gm = 512 - g; groups 0 and 256 are their
 // own partners)
 __device__ __forceinline__ int half_line(int g, int gm, int q) { return (q < HK / 2 ? g : gm) + q * HT; }
+// The split step's W^k of line q, k = half_line(g, gm, q): W^(512 q) = exp(-2 pi i q / 16) is a
+// constant of the unrolled line loop, so W^k = W^(g or gm) (two table entries per thread, loaded
+// once) times it -- no per-row table reads (r04: 16 LDS reads per thread and row, as many as
+// both of the transform's LDS transposes read)
+__device__ __forceinline__ double2 half_tw_q(double2 wb, int q) {
+    constexpr double C1 = 0.92387953251128674, S1 = 0.38268343236508978, H = 0.70710678118654752;
+    switch (q & 7) {
+    case 0: return wb;
+    case 1: return cmul(wb, make_double2(C1, -S1));
+    case 2: return cmul(wb, make_double2(H, -H));
+    case 3: return cmul(wb, make_double2(S1, -C1));
+    case 4: return make_double2(wb.y, -wb.x);  // (-i) wb
+    case 5: return cmul(wb, make_double2(-S1, -C1));
+    case 6: return cmul(wb, make_double2(-H, -H));
+    default: return cmul(wb, make_double2(-C1, -S1));
+    }
+}
 
 template <class S>
 struct Pair;  // two adjacent row elements (8-byte / 4-byte alignment: rows start at element 1)
@@ -1015,24 +1034,8 @@ struct Pair<float> {
     typedef float V __attribute__((ext_vector_type(2), aligned(4)));
 };
 
-__device__ __forceinline__ double2 half_tw(const double2 *wlo, const double2 *whi, int k) {  // W^k, k < HN
-    return cmul(wlo[k & 63], whi[k >> 6]);
-}
-
-__device__ __forceinline__ void half_lds_init(const SpecArgs &a, double2 *tw512, double2 *wlo, double2 *whi) {
-    // every load in flight before the first LDS write (one memory latency, not one per table)
-    const int t = threadIdx.x;
-    const double2 tw5 = a.tw2[t];  // W_4096^m, m < 512 (HT = 512)
-    double2 lo = make_double2(0, 0), hi = make_double2(0, 0);
-    if (t < 64) {
-        lo = a.tw[t];
-        hi = a.tw[64 * t];
-    }
-    tw512[t] = tw5;
-    if (t < 64) {
-        wlo[t] = lo;
-        whi[t] = hi;
-    }
+__device__ __forceinline__ void half_lds_init(const SpecArgs &a, double2 *tw512) {
+    tw512[threadIdx.x] = a.tw2[threadIdx.x];  // W_4096^m, m < 512 (HT = 512)
 }
 
 template <class S>
@@ -1043,14 +1046,14 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
     extern __shared__ double2 lds[];
     const HalfLds hl(lds);
     double2 *b0 = hl.b0, *b1 = hl.b1, *tw512 = hl.tw512, *stash = hl.stash;
-    double2 *wlo = hl.wlo, *whi = hl.whi;
-    half_lds_init(a, tw512, wlo, whi);
+    half_lds_init(a, tw512);
     __syncthreads();
     // the two workgroups of a chunk read the same input rows: XCD-aware order puts them on
     // one XCD (one L2) side by side
     const int wg = xcd_logical_id();
     const int t = threadIdx.x, c = wg >> 1, s = wg & 1;
     const int g = lx::mirror_group(t), gm = g == 0 ? 0 : 512 - g;
+    const double2 wg_tw = a.tw[g], wgm_tw = a.tw[gm];  // W^g, W^gm (see half_tw_q)
     const int s0 = c * a.L, e = s0 + a.L - 1;
     const int KS = a.KS;
     const int64_t ld = a.ld;
@@ -1126,6 +1129,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
         });
         lx::mirror_exchange(in, stash, tt);
         US *Urow = static_cast<US *>(a.U) + (size_t)j * 2 * KS + (size_t)s * KS;
+        double2 wb0 = wg_tw, wb1 = wgm_tw;
+        asm volatile("" : "+v"(wb0.x), "+v"(wb0.y), "+v"(wb1.x), "+v"(wb1.y));  // W^k per row, not hoisted
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
             const int k = half_line(g, gm, q);
@@ -1148,7 +1153,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passA_half(SpecArgs a) {
                 // two, so u is bit for bit the halved form's
                 const double2 E = make_double2(Zk.x + Zm.x, Zk.y - Zm.y);
                 const double2 O = make_double2(Zk.y + Zm.y, Zm.x - Zk.x);
-                const double2 X = cadd(E, cmul(half_tw(wlo, whi, k), O));
+                const double2 X = cadd(E, cmul(half_tw_q(q < HK / 2 ? wb0 : wb1, q), O));
                 const double r = RQ_HOIST ? rq[q] : scr[t + q * HT];
                 u[q] = cfma(r, u[q], cscale(X, r * csch));
                 st_u(Urow + t + q * HT, Store<S>::c(u[q]));
@@ -1188,10 +1193,10 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     extern __shared__ double2 lds[];
     const HalfLds hl(lds);
     double2 *b0 = hl.b0, *b1 = hl.b1, *tw512 = hl.tw512, *stash = hl.stash;
-    double2 *wlo = hl.wlo, *whi = hl.whi;
-    half_lds_init(a, tw512, wlo, whi);
+    half_lds_init(a, tw512);
     const int t = threadIdx.x, c = blockIdx.x;
     const int g = lx::mirror_group(t), gm = g == 0 ? 0 : 512 - g;
+    const double2 wg_tw = a.tw[g], wgm_tw = a.tw[gm];  // W^g, W^gm (see half_tw_q)
     const int L = a.L, s0 = c * L, e = s0 + L - 1;
     __shared__ double lline[64];  // L <= 64 (pick_chunk)
     __shared__ double pinw[HT / 64];
@@ -1220,6 +1225,10 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
     // the LDS tables of half_lds_init
     const double pin = pin_total<HT>(pinp, pinw);
     if (s == 0 && blockIdx.x == 0 && t == 0) a.scal[1] = pin;  // (0 when not pinned)
+    // stage 2's twiddle powers in SGPRs (lx::Stage2Tw) for B0 only: measured -4 us there, +2
+    // in B1, +4 in the 4096-point pass B, +2 in the wide-row pass A (r05i, same box)
+    std::conditional_t<SYS == 0, lx::Stage2Tw, lx::NoTw2> s2i{};
+    if constexpr (SYS == 0) s2i = lx::stage2_powers<true>(a.tw2, t);
     double2 cu[HK], w[HK];
 #pragma unroll
     for (int q = 0; q < HK; ++q) {
@@ -1285,6 +1294,8 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
         // to register q: for q >= 4 that is the partner group's register, which the mirror
         // exchange delivers.
         CX in[HK];
+        double2 wb0 = wg_tw, wb1 = wgm_tw;
+        asm volatile("" : "+v"(wb0.x), "+v"(wb0.y), "+v"(wb1.x), "+v"(wb1.y));  // W^k per row, not hoisted
 #pragma unroll
         for (int q = 0; q < HK; ++q) {
             const int k = half_line(g, gm, q);
@@ -1294,7 +1305,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
                 const double2 Xm = t == 0 ? w[(8 - q) & 7] : w[7 - q];
                 const double2 A = make_double2(w[q].x + Xm.x, w[q].y - Xm.y);
                 const double2 D = make_double2(w[q].x - Xm.x, w[q].y + Xm.y);
-                const double2 B = cmul(cconj(half_tw(wlo, whi, k)), D);
+                const double2 B = cmul(cconj(half_tw_q(q < HK / 2 ? wb0 : wb1, q)), D);
                 in[q] = make_double2(A.x - B.y, A.y + B.x);
             }
         }
@@ -1307,7 +1318,7 @@ __global__ __launch_bounds__(HT, 2) void spec_passB_half(SpecArgs a) {
         lx::fft<true, true, false>(in, b0, b1, tw512, tt, [&]() {
             if (j < e) load_u(j + 1);
             if constexpr (SYS == 1) load_y(j);
-        });
+        }, s2i);
         const CX(&xo)[HK] = in;
         // SYS 0: the next row's (r, 1/r) before this row's stores -- vmcnt counts loads and
         // stores in order, so loaded after them the next recurrence waited for every store of

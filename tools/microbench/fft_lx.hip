@@ -124,7 +124,75 @@ __global__ __launch_bounds__(T, 2) void inv_new(const double2 *in, double2 *out,
     }
 }
 
+// as the spectral passes run it: the next row prefetched during the transform (hook); ONE:
+// the one-buffer transform, half the LDS, two workgroups per CU
+template <bool ONE>
+__global__ __launch_bounds__(T, 2) void fwd_pf(const double2 *in, double2 *out, const double2 *tw, int rows, int nres) {
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *b1 = ONE ? lds : lds + N, *tw512 = lds + (ONE ? N : 2 * N), *stash = tw512 + 512;
+    lx::fill_tw512(tw512, tw);
+    __syncthreads();
+    const int t = threadIdx.x;
+    const int m = lx::mirror_group(t);
+    double2 pf[8];
+    {
+        const int j = row_of(0, rows, nres);
+#pragma unroll
+        for (int p = 0; p < 8; ++p) pf[p] = in[(size_t)j * N + t + p * T];
+    }
+    for (int i = 0; i < rows; ++i) {
+        const int j = row_of(i, rows, nres);
+        double2 v[8];
+#pragma unroll
+        for (int p = 0; p < 8; ++p) v[p] = pf[p];
+        lx::fft<false, false, true, ONE>(v, b0, b1, tw512, t, [&]() {
+            if (i + 1 < rows) {
+                const int jn = row_of(i + 1, rows, nres);
+#pragma unroll
+                for (int p = 0; p < 8; ++p) pf[p] = in[(size_t)jn * N + t + p * T];
+            }
+        });
+        lx::mirror_exchange(v, stash, t);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int k = m + q * T;
+            const double2 Zk = v[q], Zm = t == 0 ? v[(8 - q) & 7] : v[7 - q];
+            out[(size_t)j * N + k] = make_double2(Zk.x + Zm.x, Zk.y - Zm.y);
+        }
+    }
+}
+
+template <bool ONE>
+__global__ __launch_bounds__(T, 2) void inv_pf(const double2 *in, double2 *out, const double2 *tw, int rows, int nres) {
+    extern __shared__ double2 lds[];
+    double2 *b0 = lds, *b1 = ONE ? lds : lds + N, *tw512 = lds + (ONE ? N : 2 * N), *stash = tw512 + 512;
+    lx::fill_tw512(tw512, tw);
+    __syncthreads();
+    const int t = threadIdx.x;
+    const int g = lx::mirror_group(t);
+    const int gp = ((t & ~32) == 0) ? g : 512 - g;
+    double2 pf[8];
+    auto load = [&](int j) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) pf[r] = in[(size_t)j * N + (r < 4 ? g : gp) + r * T];
+    };
+    load(row_of(0, rows, nres));
+    for (int i = 0; i < rows; ++i) {
+        const int j = row_of(i, rows, nres);
+        double2 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = pf[r];
+        lx::mirror_exchange(v, stash, t);
+        lx::fft<true, true, false, ONE>(v, b0, b1, tw512, t, [&]() {
+            if (i + 1 < rows) load(row_of(i + 1, rows, nres));
+        });
+#pragma unroll
+        for (int p = 0; p < 8; ++p) out[(size_t)j * N + t + p * T] = v[p];
+    }
+}
+
 typedef void (*Kern)(const double2 *, double2 *, const double2 *, int, int);
+constexpr size_t LDS_ONE = sizeof(double2) * (lx::N + 512 + 8);
 
 int main() {
     const int WG = 256, ROWS = 64;
@@ -177,6 +245,41 @@ int main() {
     };
     if (compare(fwd_old, LDS_OLD, fwd_new, LDS_NEW, "forward+split", true)) return 1;
     if (compare(inv_old, LDS_OLD, inv_new, LDS_NEW, "inverse", false)) return 1;
+    for (auto k : {(const void *)fwd_pf<false>, (const void *)inv_pf<false>})
+        CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_NEW));
+    for (auto k : {(const void *)fwd_pf<true>, (const void *)inv_pf<true>})
+        CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_ONE));
+    if (compare(fwd_new, LDS_NEW, fwd_pf<true>, LDS_ONE, "forward+split one-buffer", true)) return 1;
+    if (compare(inv_new, LDS_NEW, inv_pf<true>, LDS_ONE, "inverse one-buffer", false)) return 1;
+    {
+        // prefetching passes: two buffers (one workgroup per CU, 256 x 64 rows) against one
+        // buffer (two per CU, 512 x 32 rows), same rows in all
+        struct P {
+            const char *name;
+            Kern k;
+            size_t lds;
+            int wg, rows;
+        } ps[] = {{"fwd_pf2", fwd_pf<false>, LDS_NEW, 256, 64}, {"fwd_pf1", fwd_pf<true>, LDS_ONE, 512, 32},
+                  {"inv_pf2", inv_pf<false>, LDS_NEW, 256, 64}, {"inv_pf1", inv_pf<true>, LDS_ONE, 512, 32}};
+        hipEvent_t f0, f1;
+        CK(hipEventCreate(&f0));
+        CK(hipEventCreate(&f1));
+        for (int rep = 0; rep < 3; ++rep)
+            for (int nres : {16, NROWS})
+                for (auto &k : ps) {
+                    k.k<<<k.wg, T, k.lds>>>(din, dout1, dtw, k.rows, nres);
+                    CK(hipEventRecord(f0));
+                    const int it = 10;
+                    for (int r = 0; r < it; ++r) k.k<<<k.wg, T, k.lds>>>(din, dout1, dtw, k.rows, nres);
+                    CK(hipEventRecord(f1));
+                    CK(hipEventSynchronize(f1));
+                    float ms = 0;
+                    CK(hipEventElapsedTime(&ms, f0, f1));
+                    const double us = ms * 1e3 / it;
+                    std::printf("rep %d %-8s rows %s: %8.1f us per launch, %6.3f us per row per CU\n", rep, k.name,
+                                nres == 16 ? "L2 " : "HBM", us, us / 64);
+                }
+    }
 
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));

@@ -40,7 +40,7 @@ body = [
         lx::fft<false, false, true>(in, b0, b1, tw512, tt, [&]() {
             STAMP(rs_ + 2);
             if (jn >= s0) load_row(jn, c1, c2);
-        });
+        }, s2f);
         asm volatile("" ::"v"(in[0].x), "v"(in[7].y));
         STAMP(rs_ + 3);'''),
     ('''                bw[q] = cfma(om[q].x, u[q], bw[q]);

@@ -1,6 +1,7 @@
-"""Phase timing of the wide-row pass A (spec_passA_half) from a stamp build
-(tools/stamps/add_stamps_half.py -> lib/exp/stampAH.so; not part of the product).  Runs 8192^2
-F32 (config 5) for a few steps and prints per-phase medians over workgroups and rows."""
+"""Phase timing from a stamp build (not part of the product): the wide-row pass A
+(tools/stamps/add_stamps_half.py -> lib/exp/stampAH.so) or the 4096-point pass B
+(add_stamps_pb4k.py -> lib/exp/stampB4.so).  Runs M^2 for a few steps and prints per-phase
+medians over workgroups and rows.  usage: stamps_phases.py M f32|f64 A|B"""
 import ctypes as C
 import os
 import sys
@@ -30,7 +31,10 @@ print("M", M, dt, "workgroups", nwg, "rows per workgroup", rows)
 print("kernel span us %.1f" % us(a[:, 255].max() - t0))
 print("start us: median %.2f max %.2f (two rounds of workgroups when > 256)" % (us(np.median(a[:, 0] - t0)), us((a[:, 0] - t0).max())))
 print("set-up us: median %.2f" % us(np.median(a[:, 1] - a[:, 0])))
-names = ["wait+projection", "stage1+T1 write", "transform rest", "split+recurrence+stores", "to next row"]
+kind = sys.argv[3] if len(sys.argv) > 3 else "A"
+names = (["wait+projection", "stage1+T1 write", "transform rest", "split+recurrence+stores", "to next row"]
+         if kind == "A" else ["u wait+convert", "recurrence (coef wait)", "exchange+transform", "stores+coef issue",
+                              "to next row"])
 ph = np.zeros((nwg, rows, 5))
 for r in range(rows):
     b = 2 + 5 * r
