@@ -2,7 +2,8 @@
 python tools/stamps/add_stamps_carry.py DIR.  Read back with tools/stamps/stamps_carry.py.
 Per workgroup (linear id x + y * gridDim.x) 8 slots: 0 entry, 1 summaries arrived (first use),
 2 segment combine done, 3 backward pass (UIN stores issued), 4 forward pass (WIN stores issued),
-5 closure (fuse_pin) done, 6 exit after the stores drained; extra-column workgroups: 0 and 6."""
+5 closure (fuse_pin) done, 6 exit after the stores drained (k-block 0 of a packed grid: after the
+extra column's work); extra-column workgroups (unpacked grids): 0 and 6."""
 import sys
 
 p = sys.argv[1] + '/qg_spectral.hip'
@@ -20,52 +21,38 @@ i0 = s.index('__global__ __launch_bounds__(64 * CARRY_WAVES, MINW) void spec_car
 i1 = s.index('// pin: cross-rank / periodic carries')
 seg = s[i0:i1]
 body = [
-    ('''    constexpr int NT = 64 * CARRY_WAVES;
-    if ((int)blockIdx.x == (a.KH + CARRY_KB - 1) / CARRY_KB) {  // the extra column''', '''    constexpr int NT = 64 * CARRY_WAVES;
+    ("""    constexpr int NT = 64 * CARRY_WAVES;
+    const bool pk = a.carry_pack != 0;""", """    constexpr int NT = 64 * CARRY_WAVES;
     STAMP(0);
-    if ((int)blockIdx.x == (a.KH + CARRY_KB - 1) / CARRY_KB) {  // the extra column'''),
-    ('''            if (threadIdx.x == 0) a.rec[rec_DSUM(a.KS)] = d;
-        }
+    const bool pk = a.carry_pack != 0;"""),
+    ("""        extra();
         return;
-    }''', '''            if (threadIdx.x == 0) a.rec[rec_DSUM(a.KS)] = d;
-        }
+    }""", """        extra();
         __builtin_amdgcn_s_waitcnt(0);
         STAMP(6);
         return;
-    }'''),
-    ('''    double2 v = make_double2(0, 0);
-    double qlen = 1;
-    if (ok) {
-        if (inreg) {''', '''    asm volatile("" ::"v"(uls[0].x), "v"(wls[CARRY_REG - 1].y));
+    }"""),
+    ("""    double2 v = make_double2(0, 0);
+    double2 qlen = make_double2(1, 1);""", """    asm volatile("" ::"v"(uls[0].x), "v"(wls[CARRY_REG - 1].y));
     STAMP(1);
     double2 v = make_double2(0, 0);
-    double qlen = 1;
-    if (ok) {
-        if (inreg) {'''),
-    ('''    for (int g = CARRY_SEG - 1; g > seg; --g) vin = cfma(qlen_s[g][kk], vin, agg[g][kk]);
+    double2 qlen = make_double2(1, 1);"""),
+    ("""        if (g > seg) vin = cfma2(qlen_s[g][kk], vin, agg[g][kk]);
     __syncthreads();
-''', '''    for (int g = CARRY_SEG - 1; g > seg; --g) vin = cfma(qlen_s[g][kk], vin, agg[g][kk]);
+""", """        if (g > seg) vin = cfma2(qlen_s[g][kk], vin, agg[g][kk]);
     __syncthreads();
     STAMP(2);
-'''),
-    ('''    agg[seg][kk] = bsum;
-    __syncthreads();''', '''    STAMP(3);
-    agg[seg][kk] = bsum;
-    __syncthreads();'''),
-    ('''    if (seg == CARRY_SEG - 1 && ok) reinterpret_cast<double2 *>(a.rec + rec_AW(KS))[s * KS + k] = w;''', '''    if (seg == CARRY_SEG - 1 && ok) reinterpret_cast<double2 *>(a.rec + rec_AW(KS))[s * KS + k] = w;
-    STAMP(4);'''),
-    ('''                if (a.pinned0) a.scal[2] = a.scal[3] = 0;  // one rank: no cross-rank line correction
-            }
-        }
-    }
-}''', '''                if (a.pinned0) a.scal[2] = a.scal[3] = 0;  // one rank: no cross-rank line correction
-            }
-        }
-    }
-    STAMP(5);
+"""),
+    ("""    agg[seg][kk] = bsum;""", """    STAMP(3);
+    agg[seg][kk] = bsum;"""),
+    ("""    if (seg == CARRY_SEG - 1 && ok) put_rec(a.rec + rec_AW(KS), s * KS, w);""", """    if (seg == CARRY_SEG - 1 && ok) put_rec(a.rec + rec_AW(KS), s * KS, w);
+    STAMP(4);"""),
+    ("""    if (pk && blockIdx.x == 0) extra();  // (packed grids: no extra column)
+}""", """    STAMP(5);
+    if (pk && blockIdx.x == 0) extra();  // (packed grids: no extra column)
     __builtin_amdgcn_s_waitcnt(0);
     STAMP(6);
-}'''),
+}"""),
 ]
 for a, b in body:
     assert seg.count(a) == 1, a[:70]
