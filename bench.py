@@ -129,13 +129,25 @@ def parse():
 PMC_KERNEL = "tendency"  # substring of the dominant kernel's name (tendency_kernel / tendency_pair_kernel)
 
 
+def pmc_counter_mean(path, ctr, kernel=PMC_KERNEL):
+    """Mean of counter `ctr` (rocprofv3 counter_collection.csv, KiB) over the dispatches of the
+    kernel whose name contains `kernel`, the first two (the Euler steps) skipped."""
+    import csv
+    v = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") == ctr and kernel in row.get("Kernel_Name", ""):
+                v.append(float(row["Counter_Value"]))
+    v = v[2:] if len(v) > 2 else v  # (the two Euler launches move less)
+    return (sum(v) / len(v), len(v)) if v else (None, 0)
+
+
 def pmc_live(args, timeout_s=150):
     """roofline.traffic of THIS run's workload: rocprofv3 --kernel-trace --pmc FETCH_SIZE, then
     WRITE_SIZE (one counter per pass, never with other traces), each a child process running 5
     steps of the same configuration; HBM bytes per launch of the dominant kernel with the
     gfx950 corrections of the MI355X guide (KiB -> bytes; FETCH_SIZE x2, WRITE_SIZE x1), the
     two Euler launches skipped.  Returns (bytes, note) or (None, reason)."""
-    import csv
     import shutil
     import signal
     import subprocess
@@ -167,15 +179,10 @@ def pmc_live(args, timeout_s=150):
             files = [os.path.join(r, f) for r, _, fs in os.walk(d) for f in fs if f.endswith("counter_collection.csv")]
             if not files:
                 return None, f"{ctr} pass wrote no counter file"
-            v = []
-            with open(files[0]) as f:
-                for row in csv.DictReader(f):
-                    if row.get("Counter_Name") == ctr and PMC_KERNEL in row.get("Kernel_Name", ""):
-                        v.append(float(row["Counter_Value"]))
-            v = v[2:] if len(v) > 2 else v  # (the two Euler launches move less)
-            if not v:
+            mean, nv = pmc_counter_mean(files[0], ctr)
+            if mean is None:
                 return None, f"{ctr}: no {PMC_KERNEL} dispatches"
-            vals[ctr] = (sum(v) / len(v) * 1024, len(v))
+            vals[ctr] = (mean * 1024, nv)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     rd, wr = 2 * vals["FETCH_SIZE"][0], vals["WRITE_SIZE"][0]
@@ -208,18 +215,19 @@ def choose_transports(qgamd, st, halo, gather, spectral):
     return "as requested"
 
 
-def verify_peer(st, torch, dist, steps=3):
+def verify_peer(st, torch, dist, steps=3, sync=None, device="cuda"):
     """The chosen peer transports against RCCL before they carry the headline (collective):
     `steps` steps from the initial state with each, every slot of zeta and psi compared bit for
     bit on every rank -- the two are bit-identical by construction
     (tests/test_gpu_rccl_multirank.py), so a stale or torn exchange between devices shows as a
     mismatch.  Leaves the peer transports set when they agree; else RCCL, and returns why."""
     halo, gather = st.halo_transport, getattr(st, "gather_transport", "rccl")
+    sync = sync or torch.cuda.synchronize
 
     def run_digest():
         st.initialise()
         st.run(1, steps)
-        torch.cuda.synchronize()
+        sync()
         return [x.detach().clone() for x in (st.zeta, st.psi)]
 
     a = run_digest()
@@ -230,7 +238,7 @@ def verify_peer(st, torch, dist, steps=3):
     iv = torch.int32 if a[0].dtype == torch.float32 else torch.int64
     same = all(torch.equal(x.view(iv), y.view(iv)) for x, y in zip(a, b))
     del a, b
-    flag = torch.tensor([0 if same else 1], dtype=torch.int32, device="cuda")
+    flag = torch.tensor([0 if same else 1], dtype=torch.int32, device=device)
     if dist is not None:
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
     if int(flag.item()):
