@@ -158,7 +158,8 @@ def pmc_live(args, timeout_s=150):
     tmp = tempfile.mkdtemp(prefix="qg_pmc_", dir="/tmp")
     env = dict(os.environ, TMPDIR="/tmp")
     child = [sys.executable, os.path.abspath(__file__), "--n", str(args.n), "--dtype", args.dtype,
-             "--dt", str(args.dt), "--steps", "5", "--warmup", "3", "--clock-warm-ms", "0",
+             "--dt", str(args.dt), "--chunk-rows", str(args.chunk_rows), "--steps", "5", "--warmup", "3",
+             "--clock-warm-ms", "0",
              "--cpu-steps", "0", "--cpu-steps-1t", "0", "--pcg-steps", "0", "--dropin-steps", "0",
              "--no-pmc-live"]
     vals = {}
