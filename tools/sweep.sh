@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/sweep
 run() {  # tag, args
   local tag=$1; shift
-  timeout -k 10 200 python bench.py --cpu-steps 0 --pcg-steps 0 --dropin-steps 0 --warmup 20 "$@" > gpurun_out/sweep/bench_$tag.json 2> gpurun_out/sweep/bench_$tag.err || return 1
+  timeout -k 10 200 python bench.py --cpu-steps 0 --cpu-steps-1t 0 --pcg-steps 0 --dropin-steps 0 --no-pmc-live --warmup 20 "$@" > gpurun_out/sweep/bench_$tag.json 2> gpurun_out/sweep/bench_$tag.err || return 1
   python -c "import json; d=json.loads(open('gpurun_out/sweep/bench_$tag.json').read().strip().splitlines()[-1]); r=d['step_roofline']; print('$tag', round(d['value'],1), round(d['ms_per_step']*1e3,1), round(r['tendency_ms']*1e3,1), round(r['solve_ms']*1e3,1), round(r['frac']*100,1))"
 }
 for n in 128 256 512 1024 2048; do run n$n --n $n --steps 2000 || exit 1; done
