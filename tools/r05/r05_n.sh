@@ -7,3 +7,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.
 tail -1 $O/smoke.log
 timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver.json 2> $O/bench_driver.err || { tail -10 $O/bench_driver.err; exit 6; }
 tail -1 $O/bench_driver.json | cut -c1-400
+timeout -k 10 400 python tools/r05/f32_scaling.py > $O/f32_scaling.txt 2>&1 || { tail -5 $O/f32_scaling.txt; exit 7; }
+cat $O/f32_scaling.txt
