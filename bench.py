@@ -45,7 +45,7 @@ def bytes_per_point(B):
     return tendency, solve, tendency + solve
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -119,11 +119,20 @@ def parse():
                          "halo overlap toggled (overlap_ab)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
+    ap.add_argument("--no-probe", dest="probe", action="store_false", default=True,
+                    help="N > 1 over RCCL: skip the peer-transport probe group (below) and let the ranks "
+                         "choose the transports themselves")
+    ap.add_argument("--probe-n", type=int, default=256,
+                    help="grid points per side per GPU of the peer-transport probe group")
+    ap.add_argument("--probe-timeout", type=float, default=180.0,
+                    help="seconds the peer-transport probe group may take before it is stopped")
+    ap.add_argument("--probe-peer", action="store_true", help=argparse.SUPPRESS)   # (a probe rank)
+    ap.add_argument("--probe-result", default=None, help=argparse.SUPPRESS)        # (launcher -> ranks)
     ap.add_argument("--no-pmc-live", dest="pmc_live", action="store_false", default=True,
                     help="N = 1: skip measuring roofline.traffic live (two rocprofv3 --pmc child runs of "
                          "this workload, FETCH_SIZE and WRITE_SIZE, ~20 s each); the committed "
                          "profiles/pmc_tendency.json is used instead")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 PMC_KERNEL = "tendency"  # substring of the dominant kernel's name (tendency_kernel / tendency_pair_kernel)
@@ -326,14 +335,16 @@ def pcg_variant(qgamd, m, n, warmup, K, torch, warm_ms=300.0):
                     "step's tendency, verdict latched there -- no host round trip)"}
 
 
-def dropin_variant(qgamd, m, n, warmup, K, torch, slot1=False):
+def dropin_variant(qgamd, m, n, warmup, K, torch, slots="all"):
     """The drop-in path: the reference's loop body on bare (M+2, P+2, 2, 3) device arrays,
     evolve_zeta!(model, zeta, psi, t, f_store) then evolve_psi!(model, zeta, psi, P, H)
     (model.jl:155, :172), each call leaving slot 1 = newest as store_new_state! does (the
-    history shifted in place on the device).  K timed steps after the warm-up.  slot1:
-    set_dropin_slots("slot1") -- slots 2-3 of zeta and psi, which the reference never reads,
-    not maintained (QG_KEEP_ORDER_SLOT1)."""
-    qgamd.set_dropin_slots("slot1" if slot1 else "all")
+    history shifted in place on the device).  K timed steps after the warm-up.  slots =
+    "slot1": set_dropin_slots("slot1") -- slots 2-3 of zeta and psi, which the reference never
+    reads, not maintained (QG_KEEP_ORDER_SLOT1); "slot1_deferred": as slot1, the new zeta's copy
+    into slot 1 done by the next evolve_psi!'s pass A (QG_KEEP_ORDER_SLOT1_DEFERRED: slot 1 of
+    zeta stale between the two calls)."""
+    qgamd.set_dropin_slots(slots)
     src = qgamd.State(m, P_local=n)
     src.initialise()
     zeta, psi, f_store = src.zeta, src.psi, src.f_store  # (heads 0 after initialise)
@@ -358,9 +369,14 @@ def dropin_variant(qgamd, m, n, warmup, K, torch, slot1=False):
     note = ("reference array signatures from Python (ctypes per call), slot order kept on every "
             "call by an in-place history shift (store_new_state!'s 2 slot copies per field; "
             "f_store's done by the AB3 tendency as it reads F(t-1), F(t-2))")
-    if slot1:
+    if slots == "slot1":
         note = ("as dropin, with slots 2-3 of zeta and psi (never read by the reference) not maintained: "
-                "the new zeta written to slot 2 and copied to slot 1, psi solved into slot 1, f_store as dropin")
+                "the new zeta written to slot 2 and copied to slot 1 by the same evolve_zeta! call (slot 1 newest "
+                "after every call), psi solved into slot 1, f_store as dropin")
+    elif slots == "slot1_deferred":
+        note = ("as dropin_slot1, the new zeta's copy into slot 1 made by the next evolve_psi!'s first solver pass "
+                "(stores only): slot 1 of zeta is stale between evolve_zeta! and evolve_psi!, where the "
+                "reference's loop never reads it")
     return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K, "note": note}
 
 
@@ -462,10 +478,110 @@ def spawn_ranks(n, argv, cmd=None, timeout_s=None):
     return rc
 
 
+# The peer transports (IPC-mapped regions written over xGMI, system-scope flags) are the N > 1
+# default, but their cross-device form has never run before the first multi-GPU node: a memory
+# fault there would kill every rank and lose the headline line.  So before the bench ranks start,
+# a probe group of the same N ranks (separate processes, separate rendezvous) sets them up at a
+# small size and checks them bit for bit against RCCL (verify_peer); the bench ranks take the
+# peer transports only if every probe rank exited 0, else RCCL, and config.transport_probe says
+# why.
+PROBE_OK, PROBE_UNAVAILABLE, PROBE_DIFFERED = 0, 3, 4
+
+
+def peer_wanted(args):
+    """Would this N > 1 RCCL run put the peer transports on its data path?"""
+    return (args.gpus > 1 and args.transport == "rccl" and
+            (args.halo != "rccl" or (args.gather != "rccl" and args.solver == "spectral")))
+
+
+def probe_verdict(rc):
+    """(peer transports usable, description) of a probe group's exit status (spawn_ranks'
+    first failing code: negative = killed by that signal, 124 = timed out)."""
+    import signal
+    if rc == PROBE_OK:
+        return True, "probe group: peer transports set up and equal to RCCL bit for bit on every rank"
+    if rc == PROBE_UNAVAILABLE:
+        return False, "probe group: peer regions unavailable on some rank"
+    if rc == PROBE_DIFFERED:
+        return False, "probe group: peer transports differed from RCCL on some rank"
+    if rc == 124:
+        return False, "probe group timed out"
+    if rc < 0:
+        try:
+            name = signal.Signals(-rc).name
+        except ValueError:
+            name = str(-rc)
+        return False, f"probe group: a rank was killed by {name}"
+    return False, f"probe group: a rank exited {rc}"
+
+
+def probe_args(ok, why):
+    """Arguments appended for the bench ranks after the probe (later flags win)."""
+    return (["--probe-result", why] if ok else ["--halo", "rccl", "--gather", "rccl", "--probe-result", why])
+
+
+def launch_self(args, argv, probe_cmd=None, rank_cmd=None):
+    """`python bench.py --gpus N` without a launcher: the probe group (when the peer transports
+    are wanted), then the N bench ranks.  The parent never touches the GPU."""
+    extra = []
+    if peer_wanted(args) and args.probe:
+        rc = spawn_ranks(args.gpus, list(argv) + ["--probe-peer"], cmd=probe_cmd, timeout_s=args.probe_timeout)
+        ok, why = probe_verdict(rc)
+        print(f"bench: {why}", file=sys.stderr, flush=True)
+        extra = probe_args(ok, why)
+    cmd = rank_cmd + extra if rank_cmd else None
+    return spawn_ranks(args.gpus, list(argv) + extra, cmd=cmd)
+
+
+def torchrun_probe(args, argv, probe_cmd=None, timeout_s=None):
+    """The probe under torch.distributed.run (the driver's multi-GPU launch): every rank, before
+    it touches the GPU, starts its probe rank as a child process; the children rendezvous on a
+    port rank 0 publishes in the launcher's own store (TORCHELASTIC_USE_AGENT_STORE), each rank
+    publishes its child's exit status there, and all ranks read all of them -- the same verdict
+    everywhere.  Without the agent's store there is nothing to agree through before RCCL
+    exists: RCCL for the headline.  Returns the extra arguments for this rank."""
+    import signal
+    import subprocess
+    from datetime import timedelta
+    from torch.distributed import TCPStore
+
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    if os.environ.get("TORCHELASTIC_USE_AGENT_STORE") != "True":
+        return probe_args(False, "no launcher store to agree on a probe through: RCCL headline")
+    timeout_s = args.probe_timeout if timeout_s is None else timeout_s
+    store = TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), is_master=False,
+                     timeout=timedelta(seconds=timeout_s + 60))
+    key = "qg_bench_probe/" + os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    if rank == 0:
+        store.set(key + "/port", str(_free_port()))
+    port = store.get(key + "/port").decode()
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    cmd = probe_cmd or [sys.executable, os.path.abspath(__file__)] + list(argv) + ["--probe-peer"]
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+    try:
+        rc = p.wait(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.wait()
+        rc = 124
+    store.set(f"{key}/rc{rank}", str(rc))
+    rcs = [int(store.get(f"{key}/rc{r}").decode()) for r in range(world)]
+    bad = [c for c in rcs if c != PROBE_OK]
+    ok, why = probe_verdict(bad[0] if bad else PROBE_OK)
+    if rank == 0:
+        print(f"bench: {why}", file=sys.stderr, flush=True)
+    return probe_args(ok, why)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(launch_self(args, sys.argv[1:]))
+    if args.gpus > 1 and not args.probe_peer and args.probe_result is None and peer_wanted(args) and args.probe:
+        # (under torch.distributed.run: the probe group first, from this rank's own child)
+        extra = torchrun_probe(args, sys.argv[1:])
+        args = parse(sys.argv[1:] + extra)
     if args.graph:
         os.environ["QG_GRAPH"] = "1"
     one_gpu = args.one_gpu and args.gpus > 1 and args.transport == "rccl"
@@ -491,7 +607,7 @@ def main():
 
     import qgamd
 
-    n = args.n
+    n = args.probe_n if args.probe_peer else args.n
     m = qgamd.bench_model(n, dt=args.dt, P=n * world)
     torch.cuda.synchronize()
     t_setup = time.perf_counter()
@@ -539,6 +655,12 @@ def main():
             st.set_overlap(overlap)
         st.initialise()
         torch.cuda.synchronize()
+    if args.probe_peer:  # (a probe rank: the verdict is the exit status)
+        peer = (cur_halo, cur_gather) != ("rccl", "rccl")
+        code = PROBE_OK if peer else (PROBE_DIFFERED if transport_check else PROBE_UNAVAILABLE)
+        del st
+        dist.destroy_process_group()
+        sys.exit(code)
 
     # the north star's PCG leg first: real work on the same grid that also brings the GPU
     # clock up before the measured model's warm-up (single GPU only)
@@ -790,6 +912,7 @@ def main():
             "halo_overlap": bool(overlap and (world > 1 or args.comm_self)),
             "transport_choice": transport_choice,
             "transport_check": transport_check,
+            "transport_probe": args.probe_result,
             "halo_transport": (cur_halo if args.transport == "rccl" and (world > 1 or args.comm_self) else None),
             "gather_transport": (cur_gather if args.transport == "rccl" and (world > 1 or args.comm_self)
                                  and args.solver == "spectral" else None),
@@ -825,9 +948,9 @@ def main():
             and not args.comm_self:
         del st
         torch.cuda.empty_cache()
-        for key, slot1 in (("dropin", False), ("dropin_slot1", True)):
+        for key, slots in (("dropin", "all"), ("dropin_slot1", "slot1"), ("dropin_slot1_deferred", "slot1_deferred")):
             try:
-                d = dropin_variant(qgamd, m, n, 3, args.dropin_steps, torch, slot1=slot1)
+                d = dropin_variant(qgamd, m, n, 3, args.dropin_steps, torch, slots=slots)
                 d["vs_qg_run_step"] = d["ms_per_step"] / ms
             except Exception as e:  # noqa: BLE001 -- reported, the headline line is still printed
                 d = {"error": f"{type(e).__name__}: {e}"}

@@ -160,13 +160,19 @@ int qg_canonicalize(qg_ctx *ctx);                   /* physically reorder to 1,2
  * on = QG_KEEP_ORDER_SLOT1 (2): slot 1 of zeta and psi and all three slots of f_store as
  * above after every call, slots 2-3 of zeta and psi NOT maintained -- the reference never
  * reads them (only evolve_zeta_layer! reads f_store's history), so its loop computes the
- * same values: no shifts of zeta and psi, the new zeta written to slot 2 and moved to slot 1
- * by the next qg_evolve_psi's first solver pass, which reads it anyway (spectral solver, power-
- * of-two M, one rank; else a slot copy at the end of qg_evolve_zeta).  Until that solve,
- * qg_slot(ctx, 0, 1, ..) names slot 2 as the newest zeta; qg_evolve_zeta, qg_synchronize,
- * qg_canonicalize and every call that moves or rebinds slots complete the move first.  Switching from QG_KEEP_ORDER_SLOT1 straight to
- * on = 1 returns QG_ERR_INVALID_ARG (slots 2-3 of zeta and psi hold stale values then).      */
+ * same values: no shifts of zeta and psi; the new zeta is written to slot 2 and copied to
+ * slot 1 at the end of qg_evolve_zeta, so slot 1 is the newest after EVERY call.
+ * on = QG_KEEP_ORDER_SLOT1_DEFERRED (3): as 2, but the copy of the new zeta into slot 1 is
+ * done by the next qg_evolve_psi's first solver pass, which reads it anyway (spectral solver,
+ * power-of-two M >= 8, one rank; else the copy of mode 2).  Between qg_evolve_zeta and that
+ * qg_evolve_psi, slot 1 of zeta is STALE: qg_slot(ctx, 0, 1, ..) names slot 2 as the newest
+ * zeta, and qg_synchronize, qg_canonicalize and every call that moves or rebinds slots
+ * complete the move first -- for callers that read zeta only after evolve_psi!, as the
+ * reference's loop does (run_model_no_output.jl:10-13).  Switching from either lean mode
+ * straight to on = 1 returns QG_ERR_INVALID_ARG (slots 2-3 of zeta and psi hold stale
+ * values then).                                                                              */
 #define QG_KEEP_ORDER_SLOT1 2
+#define QG_KEEP_ORDER_SLOT1_DEFERRED 3
 int qg_set_keep_order(qg_ctx *ctx, int on);
 int qg_get_stats(qg_ctx *ctx, qg_stats *out);
 /* PCG with the spectral preconditioner and an invertible P_fwd (the default) takes the

@@ -94,11 +94,12 @@ struct qg_ctx {
     // (model.jl:102-106), by shifting the history slots in place before the new values are
     // written; the heads then stay 0.  QG_KEEP_ORDER_SLOT1 (lean): slots 2-3 of zeta and psi,
     // which the reference never reads, are not maintained (no shifts of zeta and psi; the new
-    // zeta goes through slot 2, one slot copy)
+    // zeta goes through slot 2, one slot copy at the end of the tendency call);
+    // QG_KEEP_ORDER_SLOT1_DEFERRED: the same, the copy deferred as below
     int keep_order = 0;
-    // lean mode, single GPU, spectral solver: the new zeta waits in slot 2 (heads[0] = 1) and
-    // the next solve's pass A, which reads it anyway, writes it into slot 1 (settle_zcopy when
-    // anything else comes first)
+    // deferred lean mode, single GPU, spectral solver: the new zeta waits in slot 2 (heads[0] =
+    // 1) and the next solve's pass A, which reads it anyway, writes it into slot 1
+    // (settle_zcopy when anything else comes first)
     bool zcopy_pending = false;
     bool capturing = false;  // a step graph is being captured (no host reads, no polls)
     // deferred PCG: the latch is copied to page-locked memory every QG_PACE_STEPS steps and
@@ -423,7 +424,7 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
     // only zeta is shifted here -- zeta's slot 1 is read with a stencil and cannot be
     // overwritten in place
     const bool fuse_fshift = c->keep_order && !c->distributed && timestep >= 3;
-    const bool lean = c->keep_order == QG_KEEP_ORDER_SLOT1;
+    const bool lean = c->keep_order >= QG_KEEP_ORDER_SLOT1;
     QG_CHECK(settle_zcopy(c));  // (two tendencies in a row: the first one's zeta into slot 1 now)
     if (c->keep_order && !lean) {
         void *arr[2] = {c->zeta, c->fst};
@@ -538,7 +539,8 @@ static int evolve_zeta_t(qg_ctx *c, int64_t timestep) {
         c->ghosts_pending = true;
     }
     if (lean) {
-        if (c->spec && !c->distributed && c->spec->fuses_input_copy()) {
+        if (c->keep_order == QG_KEEP_ORDER_SLOT1_DEFERRED && c->spec && !c->distributed &&
+            c->spec->fuses_input_copy()) {
             // the next solve's pass A reads the new zeta from slot 2 and writes it into slot 1
             // (stores only; r04n's separate move read and wrote the whole field, ~0.09 ms at
             // 4096^2); meanwhile qg_slot names slot 2 as the newest
@@ -620,7 +622,7 @@ int qg_evolve_psi(qg_ctx *c) {
     const int zh = c->heads[0];
     int pn = (c->heads[1] + 2) % 3;
     if (c->keep_order) {  // store_new_state!'s shift of psi (lean: none), then the solve writes slot 1
-        if (c->keep_order != QG_KEEP_ORDER_SLOT1) {
+        if (c->keep_order < QG_KEEP_ORDER_SLOT1) {
             void *arr[1] = {c->psi};
             QG_CHECK(launch_slot_shift(arr, 1, 2 * c->esize * c->F, c->stream));
         }
@@ -784,10 +786,10 @@ int qg_canonicalize(qg_ctx *c) {
 }
 
 int qg_set_keep_order(qg_ctx *c, int on) {
-    if (!c || on < 0 || on > QG_KEEP_ORDER_SLOT1) return QG_ERR_INVALID_ARG;
-    // slots 2-3 of zeta and psi were not maintained in the lean mode: full keep-order could
+    if (!c || on < 0 || on > QG_KEEP_ORDER_SLOT1_DEFERRED) return QG_ERR_INVALID_ARG;
+    // slots 2-3 of zeta and psi were not maintained in the lean modes: full keep-order could
     // not keep its promise for the next two calls
-    if (on == 1 && c->keep_order == QG_KEEP_ORDER_SLOT1) return QG_ERR_INVALID_ARG;
+    if (on == 1 && c->keep_order >= QG_KEEP_ORDER_SLOT1) return QG_ERR_INVALID_ARG;
     QG_CHECK(settle_zcopy(c));
     if (on && !c->keep_order && c->zeta) QG_CHECK(qg_canonicalize(c));
     if (c->keep_order != on) drop_graphs(c);

@@ -118,7 +118,10 @@ static size_t coll_words(int G) { return (size_t)24 * (G + 1) + 1 + (size_t)G; }
 // ring exchange and one all-gather at a small and a large message size: every connection the
 // stepping uses is made while all ranks are known to be alive, and afterwards a silent peer
 // only leaves RCCL kernels waiting on the device, which the bounded waits abort.
-static int comm_warmup(Comm *c) {
+// `local` (this rank's set-up status so far) rides in a last all-gather, so every rank returns
+// the same verdict: a rank whose own allocations failed still takes part, and its peers learn
+// of the failure here instead of blocking later in a collective it never joins.
+static int comm_warmup(Comm *c, int local) {
     constexpr int64_t W = 131072;  // doubles: 1 MB, above every protocol's size threshold
     hipStream_t s = nullptr;
     double *buf = nullptr;
@@ -133,7 +136,20 @@ static int comm_warmup(Comm *c) {
         if (st == QG_OK && ncclAllGather(buf, buf + 4 * W, (size_t)n, ncclDouble, c->nccl, s) != ncclSuccess)
             st = QG_ERR_RCCL;
     }
+    const double mine = (double)local;  // (lives until the copy has run: comm_wait below)
+    if (st == QG_OK) {  // every rank's local status
+        if (hipMemcpyAsync(buf, &mine, sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess ||
+            ncclAllGather(buf, buf + 4 * W, 1, ncclDouble, c->nccl, s) != ncclSuccess)
+            st = QG_ERR_RCCL;
+    }
     if (st == QG_OK) st = comm_wait(c, s, nullptr, "qg_comm_init (connection warm-up)");
+    if (st == QG_OK) {
+        std::vector<double> all((size_t)c->nranks);
+        if (hipMemcpy(all.data(), buf + 4 * W, sizeof(double) * (size_t)c->nranks, hipMemcpyDeviceToHost) != hipSuccess)
+            st = QG_ERR_HIP;
+        for (int r = 0; r < c->nranks && st == QG_OK; ++r)
+            if (all[(size_t)r] != 0.0) st = (int)all[(size_t)r];
+    }
     if (buf) (void)hipFree(buf);
     (void)hipStreamDestroy(s);
     return st;
@@ -157,12 +173,17 @@ int comm_init(void **comm, int nranks, int rank, const char id[128]) {
             return QG_ERR_RCCL;
         }
     }
-    int w = comm_warmup(c);
-    if (w == QG_OK && (hipStreamCreateWithFlags(&c->coll_s, hipStreamNonBlocking) != hipSuccess ||
-                       hipMalloc((void **)&c->coll, sizeof(double) * coll_words(nranks)) != hipSuccess))
-        w = QG_ERR_HIP;
+    // the collective stream and scratch first: their status joins the warm-up's verdict
+    int local = QG_OK;
+    if (hipStreamCreateWithFlags(&c->coll_s, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc((void **)&c->coll, sizeof(double) * coll_words(nranks)) != hipSuccess) {
+        std::fprintf(stderr, "qg_mi355 rank %d/%d: allocating the collective stream / scratch failed\n", rank, nranks);
+        local = QG_ERR_ALLOC;
+    }
+    const int w = comm_warmup(c, local);
     if (w != QG_OK) {
-        std::fprintf(stderr, "qg_mi355 rank %d/%d: RCCL connection warm-up failed\n", rank, nranks);
+        if (local == QG_OK)
+            std::fprintf(stderr, "qg_mi355 rank %d/%d: RCCL connection warm-up failed (%d)\n", rank, nranks, w);
         if (c->nccl) ncclCommAbort(c->nccl);
         c->nccl = nullptr;
         if (c->progress_h) (void)hipHostFree(c->progress_h);

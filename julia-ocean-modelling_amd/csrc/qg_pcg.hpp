@@ -40,8 +40,8 @@ public:
     int iterations() const { return iters_; }
     double relres(int s) const { return relres_[s]; }
 
-    // ---- deferred certification (default; QG_PCG_SYNC=1 or qg_set_pcg_sync restores the
-    // host-checked iteration).  The certified step's residual check runs on the device and
+    // ---- deferred certification (default; qg_set_pcg_sync(ctx, 1) restores the host-checked
+    // iteration -- the library reads no environment switch for it).  The certified step's residual check runs on the device and
     // its verdict is latched there (no host round trip, graph-capturable): fused into the
     // next tendency when `fuse` (one rank), else as its own pass right after the solve.
     void set_deferred(bool on) { deferred_ = on; }

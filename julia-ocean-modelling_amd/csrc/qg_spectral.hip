@@ -2467,13 +2467,116 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
 
 // power-of-two rows 8 .. 8192 (FFT passes), any other rows 3 .. GEN_MMAX (generic passes)
 // and GEN_MMAX .. SPL_MMAX (split passes), even rows to SPL_WMAX (wide split passes), any row
+// ---- two-point domains (global M = 2 or P = 2, one rank) --------------------------------
+// The reference's 1-D periodic operator is laplacian_1d with the wrap entries written over it
+// (laplacian.jl:40-45).  For N = 2 the wrap entries ARE the neighbour entries, so its D_2 is
+// [-2 1; 1 -2] -- eigenvalue -1 on (1, 1), -3 on (1, -1) -- not the periodic 5-point operator's
+// [-2 2; 2 -2] that the FACR passes diagonalise.  Solved here as the reference builds it
+// (construct_spA, laplacian.jl:54-58): in the modes q of the two-point direction
+// (X_q = x_a + x_b, x_a - x_b) the system (L + alpha dx^2) x = dx^2 zeta~ separates into one
+// line along the other direction per (system, mode), (D_N + c_q) X_q = R_q with
+// c_q = lambda_q + alpha dx^2 <= -1: cyclic tridiagonal (diagonal a = -(r + 1/r), both
+// neighbours 1) for N >= 3, solved exactly as X = -r (1 - r S+)^-1 (1 - r S-)^-1 R with the
+// periodic closures of the two first-order filters, or the 2 x 2 [a 1; 1 a] for N = 2.  Both
+// systems are nonsingular, so the pinned Poisson system of get_poisson_cholesky (row and column
+// of point 1 -> identity, b[1] = 0; laplacian.jl:66-75, model.jl:185) is the unpinned solution y
+// plus the multiple of z = A0^-1 e_1 that zeroes point 1: x = y - (y_1 / z_1) z (only the first
+// equation is dropped, so A x = b + mu e_1 with x_1 = 0).  z is solved once at init by the same
+// kernel (unit = 1).  One workgroup: four threads run the lines, then all threads combine the
+// modes, pin, back-project and write the ghost ring.  No performance at stake (a test domain).
+template <class S>
+__global__ __launch_bounds__(256) void spec_twopoint(SpecArgs a, int unit) {
+    const int64_t M = a.M, P = a.P, ld = a.ld, N = a.two_N;
+    const double dx2 = a.dx * a.dx;
+    // line point n, two-point index t -> interior (i, j)
+    auto idx = [&](int64_t n, int t) -> int64_t {
+        return a.two_yline ? fidx(1 + t, n + 1, ld) : fidx(n + 1, 1 + t, ld);
+    };
+    const S *in1 = static_cast<const S *>(a.in1), *in2 = static_cast<const S *>(a.in2);
+    if (threadIdx.x < 4) {
+        const int s = threadIdx.x >> 1, q = threadIdx.x & 1;
+        double *X = a.two_X + (size_t)(2 * s + q) * N;
+        if (!unit || s == 0) {
+            const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];
+            auto zt = [&](int64_t n, int t) -> double {
+                if (s == 0 && a.pinned0 && n == 0 && t == 0) return 0.0;  // b[1] = 0
+                const int64_t o = idx(n, t);
+                return pa * (double)in1[o] + pb * (double)in2[o];
+            };
+            // right-hand side of mode q: dx^2 (zeta~_a +- zeta~_b); unit: -dx^2 e_1 in both modes
+            auto R = [&](int64_t n) -> double {
+                if (unit) return n == 0 ? -dx2 : 0.0;
+                const double v0 = zt(n, 0), v1 = zt(n, 1);
+                return dx2 * (q == 0 ? v0 + v1 : v0 - v1);
+            };
+            const double r = a.two_r[s][q];
+            if (N == 2) {  // [a 1; 1 a]^-1 = [a -1; -1 a] / (a^2 - 1), a = two_r
+                const double r0 = R(0), r1 = R(1), den = r * r - 1.0;
+                X[0] = (r * r0 - r1) / den;
+                X[1] = (r * r1 - r0) / den;
+            } else {
+                // w = (1 - r S-)^-1 R: w_n = R_n + r w_{n-1}, w_0 = sum_m r^m R_{-m} / (1 - r^N)
+                double acc = 0.0, pw = 1.0;
+                for (int64_t m = 0; m < N && pw != 0.0; ++m) {
+                    acc += pw * R((N - m) % N);
+                    pw *= r;
+                }
+                X[0] = acc * a.two_inv1mrN[s][q];
+                for (int64_t n = 1; n < N; ++n) X[n] = R(n) + r * X[n - 1];
+                // v = (1 - r S+)^-1 w: v_n = w_n + r v_{n+1}, v_{N-1} = sum_m r^m w_{N-1+m} / (1 - r^N)
+                acc = 0.0;
+                pw = 1.0;
+                for (int64_t m = 0; m < N && pw != 0.0; ++m) {
+                    acc += pw * X[(N - 1 + m) % N];
+                    pw *= r;
+                }
+                double v = acc * a.two_inv1mrN[s][q];
+                X[N - 1] = -r * v;
+                for (int64_t n = N - 2; n >= 0; --n) {
+                    v = X[n] + r * v;
+                    X[n] = -r * v;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const double *X = a.two_X;
+    auto sol = [&](int s, int64_t n, int t) -> double {
+        const double p = X[(size_t)(2 * s) * N + n], m = X[(size_t)(2 * s + 1) * N + n];
+        return 0.5 * (t == 0 ? p + m : p - m);
+    };
+    if (unit) {
+        for (int64_t e = threadIdx.x; e < 2 * N; e += blockDim.x) a.two_z[e] = sol(0, e >> 1, (int)(e & 1));
+        return;
+    }
+    const double y1 = sol(0, 0, 0);
+    const double mu = a.pinned0 ? y1 / a.two_z[0] : 0.0;
+    if (threadIdx.x == 0) {
+        a.scal[0] = 0.0;  // no compatibility shift: both systems are nonsingular
+        a.scal[1] = y1;   // the unpinned solution at point 1, removed by the pin
+    }
+    S *out1 = static_cast<S *>(a.out1), *out2 = static_cast<S *>(a.out2);
+    const int64_t tot = (M + 2) * (P + 2);
+    for (int64_t e = threadIdx.x; e < tot; e += blockDim.x) {
+        const int64_t gi = e % (M + 2), gj = e / (M + 2);
+        const int64_t i = ((gi - 1) % M + M) % M, j = ((gj - 1) % P + P) % P;  // periodic ghosts
+        const int64_t n = a.two_yline ? j : i;
+        const int t = (int)(a.two_yline ? i : j);
+        double x0 = sol(0, n, t);
+        if (a.pinned0) x0 -= mu * a.two_z[2 * n + t];
+        const double x1 = sol(1, n, t);
+        out1[gi + ld * gj] = (S)(a.pin_out[0] * x0 + a.pin_out[1] * x1);
+        if (out2) out2[gi + ld * gj] = (S)(a.pin_out[2] * x0 + a.pin_out[3] * x1);
+    }
+}
+
 // beyond (odd above SPL_MMAX, or above SPL_WMAX) up to BL_MMAX (Bluestein rows)
 static bool bluestein_rows(int64_t M) { return M > SPL_WMAX || (M > SPL_MMAX && M % 2 != 0); }
 bool SpectralSolver::supports(int64_t M, int64_t P) {
     if (P < 2) return false;
     if (M >= 8 && M <= 8192 && (M & (M - 1)) == 0) return true;
     if (M > SPL_MMAX) return M <= BL_MMAX;
-    return M >= 3 && M <= SPL_MMAX;
+    return M >= 2 && M <= SPL_MMAX;  // (M = 2: the two-point path, one rank)
 }
 
 // Bluestein tables (long double on the host): the chirp, and the filter's length-L transform
@@ -2546,12 +2649,11 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
                          int chunk_rows, int f32) {
     if (!supports(M, P)) return QG_ERR_UNSUPPORTED;
     if (!(dx > 0) || nranks < 1 || rank < 0 || rank >= nranks || P_total != P * nranks) return QG_ERR_INVALID_ARG;
-    // two rows in all: the reference's laplacian_1d_periodic (laplacian.jl:41-46) writes its
-    // wrap entry over the neighbour entry (lap[1, end] = 1 where both neighbours of a row are
-    // the same row), so its matrix is not the periodic 5-point operator its tendency applies;
-    // refused rather than solving a different system (the C oracle, like this solver, would
-    // solve the periodic one: 0.28 relative residual against the reference's matrix)
-    if (P_total < 3) return QG_ERR_UNSUPPORTED;
+    // two points in a direction (global): the reference's laplacian_1d_periodic
+    // (laplacian.jl:40-45) writes its wrap entry over the neighbour entry, so its matrix is not
+    // the periodic 5-point operator the passes below diagonalise -- solved as the reference
+    // builds it by spec_twopoint (one rank: a two-row domain split over ranks has one-row slabs)
+    if (M == 2 || P_total == 2) return init_twopoint(M, P, nranks, dx, alpha, pinned0, pin_in, pin_out, f32);
     const int L = pick_chunk(M, P, chunk_rows);
     if (L < 1) return QG_ERR_INVALID_ARG;
     SpecArgs &a = a_;
@@ -2765,6 +2867,60 @@ int SpectralSolver::init(int64_t M, int64_t P, int64_t P_total, int rank, int nr
     return QG_OK;
 }
 
+int SpectralSolver::init_twopoint(int64_t M, int64_t P, int nranks, double dx, const double alpha[2], int pinned0,
+                                  const double pin_in[4], const double pin_out[4], int f32) {
+    if (nranks != 1) return QG_ERR_UNSUPPORTED;
+    SpecArgs &a = a_;
+    a.M = M;
+    a.P = P;
+    a.ld = M + 2;
+    a.P_total = P;
+    a.rank = 0;
+    a.nranks = 1;
+    a.f32 = f32;
+    a.dx = dx;
+    a.pinned0 = pinned0 ? 1 : 0;
+    std::memcpy(a.pin_in, pin_in, sizeof(a.pin_in));
+    std::memcpy(a.pin_out, pin_out, sizeof(a.pin_out));
+    a.two = 1;
+    a.two_yline = P != 2 ? 1 : 0;  // (M = P = 2: the line along x, of two points)
+    const int64_t N = a.two_yline ? P : M;
+    a.two_N = N;
+    const long double lam[2] = {-1.0L, -3.0L};  // D_2 on (1, 1) and (1, -1)
+    for (int s = 0; s < 2; ++s)
+        for (int q = 0; q < 2; ++q) {
+            const long double c = lam[q] + (long double)alpha[s] * (long double)dx * (long double)dx;
+            if (!(c < 0)) return QG_ERR_UNSUPPORTED;  // (alpha > 0: not the reference's systems)
+            if (N == 2) {
+                a.two_r[s][q] = (double)(c - 2);  // the diagonal a of [a 1; 1 a]
+                a.two_inv1mrN[s][q] = 0;
+            } else {
+                const long double rho = 1 - c / 2;  // > 1
+                const long double r = 1 / (rho + sqrtl((rho - 1) * (rho + 1)));
+                a.two_r[s][q] = (double)r;
+                a.two_inv1mrN[s][q] = (double)(-1 / expm1l((long double)N * logl(r)));
+            }
+        }
+    const size_t n_X = align_up(sizeof(double) * 4 * (size_t)N), n_z = align_up(sizeof(double) * 2 * (size_t)N);
+    const size_t n_scal = align_up(sizeof(double) * 8);
+    bytes_ = n_X + n_z + n_scal;
+    if (hipMalloc(&mem_, bytes_) != hipSuccess) {
+        mem_ = nullptr;
+        return QG_ERR_ALLOC;
+    }
+    char *p = static_cast<char *>(mem_);
+    a.two_X = (double *)p;
+    a.two_z = (double *)(p + n_X);
+    a.scal = (double *)(p + n_X + n_z);
+    QG_HIP(hipMemset(mem_, 0, bytes_));
+    if (a.pinned0) {  // z = A0^-1 e_1, once
+        spec_twopoint<double><<<1, 256, 0, nullptr>>>(a, 1);
+        QG_LAUNCH_CHECK();
+        QG_HIP(hipStreamSynchronize(nullptr));
+    }
+    return QG_OK;
+}
+
 SpectralSolver::~SpectralSolver() {
     if (mem_) (void)hipFree(mem_);
 }
@@ -2784,6 +2940,12 @@ int SpectralSolver::solve(const void *in1, const void *in2, void *out1, void *ou
     a.out1 = out1;
     a.out2 = out2;
     a.write_ghost_rows = write_ghost_rows;
+    if (a.two) {
+        if (a.f32) spec_twopoint<float><<<1, 256, 0, s>>>(a, 0);
+        else spec_twopoint<double><<<1, 256, 0, s>>>(a, 0);
+        QG_LAUNCH_CHECK();
+        return QG_OK;
+    }
     // one rank: the carry kernel closes the lines itself (no spec_pin), with or without a
     // transport -- a 1-rank ring's record all-gather would only copy the record onto itself
     // (grec aliases rec), so none is posted (r04: RCCL's one-rank all-gather was a 6 us copy

@@ -89,6 +89,14 @@ struct SpecArgs {
     // (single GPU) -- the drop-in lean mode's move of the new zeta into slot 1 (qg_capi.hip)
     void *zcopy1, *zcopy2;
     int npin;                 // pin parts pass B sums (pinpart[0 .. npin))
+    // two-point domains (global M = 2 or P = 2, one rank): see spec_twopoint
+    int two;                  // 1: this solver is the two-point path
+    int two_yline;            // 1: the line runs along y (M = 2, P >= 3), else along x (P = 2)
+    int64_t two_N;            // line length
+    double two_r[2][2];       // [system][mode] filter root r (N >= 3) or diagonal a (N = 2)
+    double two_inv1mrN[2][2]; // 1 / (1 - r^N)
+    double *two_X;            // [2][2][N] line solutions
+    double *two_z;            // [N][2] A0^-1 e_1 of the unpinned Poisson operator (the pin)
 };
 
 // record layout (doubles)
@@ -115,12 +123,14 @@ public:
               const double *pin_out = nullptr,  // optional per-call projections
               void *zcopy1 = nullptr, void *zcopy2 = nullptr);  // see SpecArgs::zcopy1
     // pass A can write the zcopy fields (power-of-two rows: the FFT and wide-row passes)
-    bool fuses_input_copy() const { return a_.M >= 8 && a_.M <= 8192 && (a_.M & (a_.M - 1)) == 0; }
+    bool fuses_input_copy() const { return !a_.two && a_.M >= 8 && a_.M <= 8192 && (a_.M & (a_.M - 1)) == 0; }
     const SpecArgs &args() const { return a_; }
     size_t device_bytes() const { return bytes_; }
     double *gather_buf() const { return grec_buf_; }  // the record all-gather's target
 
 private:
+    int init_twopoint(int64_t M, int64_t P, int nranks, double dx, const double alpha[2], int pinned0,
+                      const double pin_in[4], const double pin_out[4], int f32);
     SpecArgs a_{};
     void *mem_ = nullptr;
     double *grec_buf_ = nullptr;

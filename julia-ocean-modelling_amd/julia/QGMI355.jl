@@ -154,15 +154,21 @@ evolve_psi!(model, s::QGState, poisson=nothing, helmholtz=nothing) =
 const _BOUND = Dict{NTuple{3,UInt},QGState}()
 # slots maintained on arrays bound from now on: 1 = all (store_new_state! exactly), 2 =
 # QG_KEEP_ORDER_SLOT1 (slot 1 of zeta / psi and all of f_store: the values the reference's
-# loop reads; one slot copy per step instead of four)
+# loop reads, newest after every call; one slot copy per step instead of four), 3 =
+# QG_KEEP_ORDER_SLOT1_DEFERRED (as 2, the new zeta's copy into slot 1 done by the next
+# evolve_psi!: slot 1 of zeta is stale between evolve_zeta! and evolve_psi!)
 const _DROPIN_SLOTS = Ref{Cint}(1)
 
-"""`set_dropin_slots!(:all | :slot1)`: the slots the reference-signature calls maintain on
-arrays bound from now on (`:slot1` leaves slots 2-3 of `zeta` / `psi`, which the reference
-never reads, unmaintained)."""
+"""`set_dropin_slots!(:all | :slot1 | :slot1_deferred)`: the slots the reference-signature
+calls maintain on arrays bound from now on.  `:slot1` leaves slots 2-3 of `zeta` / `psi`,
+which the reference never reads, unmaintained; slot 1 is the newest after every call.
+`:slot1_deferred` also defers the copy of the new `zeta` into slot 1 to the next
+`evolve_psi!` (its first solver pass reads that field anyway): `zeta[:, :, :, 1]` must not be
+read between `evolve_zeta!` and `evolve_psi!` (`synchronize(s)` completes the move)."""
 function set_dropin_slots!(mode::Symbol)
-    mode in (:all, :slot1) || throw(ArgumentError("mode must be :all or :slot1"))
-    _DROPIN_SLOTS[] = mode === :slot1 ? Cint(2) : Cint(1)
+    mode in (:all, :slot1, :slot1_deferred) ||
+        throw(ArgumentError("mode must be :all, :slot1 or :slot1_deferred"))
+    _DROPIN_SLOTS[] = mode === :slot1 ? Cint(2) : mode === :slot1_deferred ? Cint(3) : Cint(1)
     mode
 end
 

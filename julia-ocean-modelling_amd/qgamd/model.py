@@ -390,14 +390,18 @@ class State:
     def canonicalize(self):
         call("qg_canonicalize", self._ctx)
 
-    def set_keep_order(self, on=True, slot1_only=False):
+    def set_keep_order(self, on=True, slot1_only=False, deferred=False):
         """qg_set_keep_order: every call leaves slot 1 = newest (store_new_state!'s shift, in
         place, before the new values are written), so the arrays are always in the
         reference's slot order; off (default) rotates the slots instead.  slot1_only
-        (QG_KEEP_ORDER_SLOT1): slot 1 of zeta / psi and all of f_store kept so, slots 2-3 of
-        zeta and psi (never read by the reference) not maintained -- one slot copy per step
-        instead of four."""
-        call("qg_set_keep_order", self._ctx, (2 if slot1_only else 1) if on else 0)
+        (QG_KEEP_ORDER_SLOT1): slot 1 of zeta / psi and all of f_store kept so after every
+        call, slots 2-3 of zeta and psi (never read by the reference) not maintained -- one
+        slot copy per step instead of four.  deferred (with slot1_only,
+        QG_KEEP_ORDER_SLOT1_DEFERRED): that copy rides in the next evolve_psi!'s first solver
+        pass, so slot 1 of zeta is stale between evolve_zeta! and evolve_psi! (qg_slot names
+        the newest; synchronize() completes the move)."""
+        mode = (_lib.QG_KEEP_ORDER_SLOT1_DEFERRED if deferred else _lib.QG_KEEP_ORDER_SLOT1) if slot1_only else 1
+        call("qg_set_keep_order", self._ctx, mode if on else 0)
 
     def to_numpy(self, which):
         """Reference-ordered numpy array of shape (M+2, P+2, 2, 3) (Julia index order).
@@ -417,17 +421,20 @@ def initialise_model(m, seeds=(SEED_LAYER1, SEED_LAYER2), **kw):
 
 
 _BOUND = {}
-_DROPIN_SLOT1_ONLY = [False]
+_DROPIN_SLOTS = ["all"]
 
 
 def set_dropin_slots(mode):
     """Slots the reference-signature calls below maintain on arrays bound from now on:
-    "all" (default: store_new_state! exactly, slots 2-3 of zeta and psi shifted too) or
+    "all" (default: store_new_state! exactly, slots 2-3 of zeta and psi shifted too),
     "slot1" (QG_KEEP_ORDER_SLOT1: slot 1 of zeta and psi and all of f_store, the values the
-    reference's loop reads; one slot copy per step instead of four)."""
-    if mode not in ("all", "slot1"):
-        raise ValueError("mode must be 'all' or 'slot1'")
-    _DROPIN_SLOT1_ONLY[0] = mode == "slot1"
+    reference's loop reads, newest after every call; one slot copy per step instead of four)
+    or "slot1_deferred" (QG_KEEP_ORDER_SLOT1_DEFERRED: as "slot1", the copy of the new zeta
+    into slot 1 done by the next evolve_psi!'s first solver pass -- slot 1 of zeta is stale
+    between evolve_zeta! and evolve_psi!, which the reference's loop never reads there)."""
+    if mode not in ("all", "slot1", "slot1_deferred"):
+        raise ValueError("mode must be 'all', 'slot1' or 'slot1_deferred'")
+    _DROPIN_SLOTS[0] = mode
 
 
 def _bound_state(m, zeta, psi, f_store):
@@ -442,7 +449,8 @@ def _bound_state(m, zeta, psi, f_store):
             st = None
             unbind(zeta, psi, f_store)
         st = _BOUND[key] = State(m, device=zeta.device, dtype=zeta.dtype, arrays=(zeta, psi, f_store))
-        st.set_keep_order(True, slot1_only=_DROPIN_SLOT1_ONLY[0])
+        st.set_keep_order(True, slot1_only=_DROPIN_SLOTS[0] != "all",
+                          deferred=_DROPIN_SLOTS[0] == "slot1_deferred")
     return st
 
 

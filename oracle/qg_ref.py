@@ -253,6 +253,42 @@ def get_poisson_cholesky(M, P, dx):  # laplacian.jl:66-75
     return _Factor(_pin_first(-construct_spA(M, P, dx, 0.0)))
 
 
+def solve_longdouble(M, P, dx, alpha, f, pinned=False, workers=None):
+    """Extended-precision reference solve (x86 80-bit long double, eps = 5.4e-20) of the same
+    systems: construct_spA(M, P, dx, alpha) x = f over the interior of the (M+2, P+2) field f
+    (laplacian.jl:54-58, M, P >= 3), or with ``pinned`` the pinned Poisson system of
+    get_poisson_cholesky (laplacian.jl:66-75, b[1] = 0 as model.jl:185): the compatible
+    right-hand side f - sum(f) e_1, the mean-free DFT solve, minus its value at point 1 --
+    the pinned solution exactly (the pin drops only the first equation).  2-D DFT by
+    scipy.fft in long double, eigenvalues -4 dx^-2 (sin^2(pi kx / M) + sin^2(pi ky / P)) +
+    alpha in the cancellation-free form.  Not an F64 solver: it measures how far each F64
+    solver (the C oracle, the device) is from the exact solution of the F64 input, so that
+    the difference between two of them can be attributed."""
+    import scipy.fft as sfft
+    ld = np.longdouble
+    g = np.asarray(f, dtype=np.float64)[1:-1, 1:-1].astype(ld)
+    if pinned:
+        g[0, 0] -= np.sum(g)  # (pairwise summation in long double)
+    G = sfft.fft2(g, workers=workers)
+    del g
+    pi = ld("3.14159265358979323846264338327950288")
+    sx = np.sin(pi * np.arange(M, dtype=ld) / ld(M)) ** 2
+    sy = np.sin(pi * np.arange(P, dtype=ld) / ld(P)) ** 2
+    lam = (ld(-4) / (ld(dx) * ld(dx))) * (sx[:, None] + sy[None, :]) + ld(alpha)
+    if pinned:
+        lam[0, 0] = 1
+        G[0, 0] = 0
+    G /= lam
+    del lam
+    x = sfft.ifft2(G, workers=workers).real
+    del G
+    if pinned:
+        x -= x[0, 0]
+    out = np.zeros((M + 2, P + 2), dtype=ld)
+    out[1:-1, 1:-1] = x
+    return update_doubly_periodic_bc(out)
+
+
 def _vec(a):
     """Julia vec: column-major flatten (i fastest)."""
     return np.asarray(a).flatten(order="F")

@@ -71,4 +71,93 @@ def test_bench_main_spawns_when_world_size_is_unset(monkeypatch):
         bench.main()
     except SystemExit as e:
         assert e.code == 0
-    assert calls == [(4, ["--gpus", "4", "--steps", "7"])]
+    # the probe group, then the bench ranks with its verdict
+    assert calls[0] == (4, ["--gpus", "4", "--steps", "7", "--probe-peer"])
+    assert calls[1][0] == 4 and calls[1][1][:4] == ["--gpus", "4", "--steps", "7"]
+    assert calls[1][1][4] == "--probe-result" and len(calls) == 2
+
+
+# ---- the peer-transport probe group ----------------------------------
+_SEGV = "import os, signal\nos.kill(os.getpid(), signal.SIGSEGV)\n"
+_RANK_ECHO = """
+import json, os, sys
+if os.environ["RANK"] == "0":
+    print("HEADLINE " + json.dumps(sys.argv[1:]), flush=True)
+"""
+
+
+def test_probe_killed_by_sigsegv_falls_back_to_rccl(capfd):
+    """A probe rank that dies by SIGSEGV (what a fault in the cross-device IPC path would do)
+    stops the probe group; the bench ranks are then started with the RCCL transports and the
+    reason, and rank 0 still prints its line."""
+    args = bench.parse(["--gpus", "2"])
+    assert bench.peer_wanted(args)
+    rc = bench.launch_self(args, ["--gpus", "2"], probe_cmd=[sys.executable, "-c", _SEGV],
+                           rank_cmd=[sys.executable, "-c", _RANK_ECHO])
+    assert rc == 0
+    out = capfd.readouterr()
+    line = [x for x in out.out.splitlines() if x.startswith("HEADLINE ")]
+    assert len(line) == 1
+    argv = json.loads(line[0][len("HEADLINE "):])
+    got = bench.parse(["--gpus", "2"] + argv)
+    assert (got.halo, got.gather) == ("rccl", "rccl")
+    assert "SIGSEGV" in got.probe_result and "SIGSEGV" in out.err
+
+
+def test_probe_success_keeps_the_peer_transports(capfd):
+    args = bench.parse(["--gpus", "2"])
+    rc = bench.launch_self(args, ["--gpus", "2"], probe_cmd=[sys.executable, "-c", "pass"],
+                           rank_cmd=[sys.executable, "-c", _RANK_ECHO])
+    assert rc == 0
+    line = [x for x in capfd.readouterr().out.splitlines() if x.startswith("HEADLINE ")][0]
+    got = bench.parse(["--gpus", "2"] + json.loads(line[len("HEADLINE "):]))
+    assert (got.halo, got.gather) == ("auto", "auto") and got.probe_result.startswith("probe group: peer")
+
+
+def test_probe_verdicts():
+    assert bench.probe_verdict(0)[0]
+    for rc, word in ((3, "unavailable"), (4, "differed"), (124, "timed out"), (-6, "SIGABRT"), (-11, "SIGSEGV"),
+                     (1, "exited 1")):
+        ok, why = bench.probe_verdict(rc)
+        assert not ok and word in why, (rc, why)
+    # an RCCL-only run, or --no-probe, starts no probe group
+    assert not bench.peer_wanted(bench.parse(["--gpus", "2", "--halo", "rccl", "--gather", "rccl"]))
+    assert not bench.peer_wanted(bench.parse(["--gpus", "1"]))
+
+
+_TORCHRUN_RANK = """
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+import bench
+bad = sys.argv[3]
+probe = [sys.executable, "-c", "import os, signal\\nif os.environ['RANK'] == %r: os.kill(os.getpid(), signal.SIGSEGV)\\n" % bad]
+extra = bench.torchrun_probe(bench.parse(["--gpus", "2"]), ["--gpus", "2"], probe_cmd=probe, timeout_s=60)
+open(os.path.join(sys.argv[2], "r%s.json" % os.environ["RANK"]), "w").write(json.dumps(extra))
+"""
+
+
+def _torchrun(tmp_path, bad_rank):
+    import subprocess
+    script = tmp_path / "rank.py"
+    script.write_text(_TORCHRUN_RANK)
+    port = bench._free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), str(script), ROOT, str(tmp_path), bad_rank]
+    subprocess.run(cmd, check=True, timeout=180, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    return [json.loads((tmp_path / f"r{r}.json").read_text()) for r in range(2)]
+
+
+def test_torchrun_probe_fault_on_one_rank_moves_every_rank_to_rccl(tmp_path):
+    """Under torch.distributed.run: rank 1's probe child dies by SIGSEGV; both ranks learn it
+    through the launcher's store and both get the RCCL transports (the same verdict everywhere)."""
+    extra = _torchrun(tmp_path, "1")
+    for e in extra:
+        got = bench.parse(["--gpus", "2"] + e)
+        assert (got.halo, got.gather) == ("rccl", "rccl") and "SIGSEGV" in got.probe_result
+
+
+def test_torchrun_probe_success_on_every_rank(tmp_path):
+    extra = _torchrun(tmp_path, "none")
+    for e in extra:
+        got = bench.parse(["--gpus", "2"] + e)
+        assert (got.halo, got.gather) == ("auto", "auto") and "bit for bit" in got.probe_result

@@ -117,6 +117,75 @@ def test_config4_global_grid_against_c_oracle(env, capsys):
         assert e < 1e-10, (n, e)
 
 
+@pytest.mark.parametrize("G", [2, 8])
+def test_weak_scaling_global_grids_against_c_oracle(env, G, capsys):
+    """The global grids of bench.py --gpus 2 and --gpus 8 (4096 x 8192, 4096 x 32768 F64: the
+    weak-scaling points SCALE reports) on one GPU against the C oracle: 3 steps, psi and zeta
+    (slot 1) < 1e-10 relative RMS, the north-star tolerance.  The long
+    y-extent makes the pinned Poisson problem's gravest modes (eigenvalues ~ (2 pi / P)^2)
+    amplify any solver's roundoff: the C oracle's old eigenvalue expression lost them to
+    cancellation (device vs oracle 4.5e-11 at 4096 x 16384, growing with P); with the
+    cancellation-free form both solvers are within ~1e-12 of the long-double solve
+    (test_device_solve_against_longdouble_on_long_grids)."""
+    torch, qgamd, _ = env
+    from oracle import qg_oracle as O
+    from oracle import qg_ref as R
+
+    N, steps = 4096, 3
+    st = qgamd.run_model_no_output(qgamd.bench_model(N, P=G * N, dt=60.0), nsteps=steps)
+    st.synchronize()
+    got = {n: np.stack([st.current(n, l).cpu().numpy().T for l in (1, 2)], axis=-1) for n in ("psi", "zeta")}
+    del st
+    torch.cuda.empty_cache()
+    ref = O.State(R.bench_model(N, P=G * N, dt=60.0)).run(steps)
+    for n in ("psi", "zeta"):
+        want = getattr(ref, n)[:, :, :, 0]
+        e = np.linalg.norm(got[n] - want) / np.linalg.norm(want)
+        with capsys.disabled():
+            print(f"\nglobal 4096x{G * N} vs C oracle, {steps} steps, {n}: {e:.3e}")
+        assert e < 1e-10, (n, e)
+
+
+@pytest.mark.parametrize("P", [8192, 16384, 32768])
+def test_device_solve_against_longdouble_on_long_grids(env, P, capsys):
+    """The device's direct solve of evolve_psi!'s two systems on the weak-scaling grids
+    (4096 x 2, 4 and 8 slabs' rows) against the extended-precision solve of the same F64
+    right-hand side (oracle/qg_ref.solve_longdouble, long double, eps 5.4e-20): the pinned
+    Poisson solution < 1e-11 and the Helmholtz one < 1e-13 relative, so the device's own
+    error is two orders below the north-star 1e-10 and the trajectory tests above measure the
+    oracle's and the device's roundoff together, not a conditioning floor."""
+    torch, qgamd, _ = env
+    from oracle import qg_ref as R
+
+    M = 4096
+    dx = 4e6 / M
+    f = R.update_doubly_periodic_bc(R.seeded_rand(M, P, 17) - 0.5) * 1e-9
+    t = torch.from_numpy(np.ascontiguousarray(f.T)).cuda()
+    for alpha, pinned, bar in ((0.0, True, 1e-11), (-6.25e-10, False, 1e-13)):
+        got = (qgamd.sp_solve_poisson(M, P, dx, t) if pinned
+               else qgamd.sp_solve_modified_helmholtz(M, P, dx, t, alpha)).cpu().numpy().T
+        x = R.solve_longdouble(M, P, dx, alpha, f, pinned=pinned, workers=16)
+        e = float(np.linalg.norm((got - x)[1:-1, 1:-1]) / np.linalg.norm(x[1:-1, 1:-1]))
+        del x, got
+        with capsys.disabled():
+            print(f"\ndevice solve {M}x{P} {'poisson' if pinned else 'helmholtz'} vs long double: {e:.3e}")
+        assert e < bar, (P, pinned, e)
+
+
+def test_config_g8_eight_4096_slabs(env, capsys):
+    """Eight 4096^2 F64 slabs (the --gpus 8 weak-scaling workload, global 4096 x 32768) over the
+    in-process transport against one GPU on the global grid: every slot < 1e-10."""
+    torch, qgamd, ThreadRing = env
+    G, N, steps = 8, 4096, 4
+    m = qgamd.bench_model(N, P=G * N, dt=60.0)
+    glob = qgamd.run_model_no_output(m, nsteps=steps)
+    torch.cuda.synchronize()
+    slabs = _run_slabs(torch, qgamd, ThreadRing, m, G, steps, torch.float64)
+    worst = _compare_slabs(torch, glob, slabs, 1e-10)
+    with capsys.disabled():
+        print(f"\n8 x 4096^2 F64 slabs vs one GPU ({steps} steps): worst rel diff {worst}")
+
+
 # F32 state vs the F64 device path (pinned to the oracle) at config 5's 8192^2: relative RMS of
 # psi and zeta (slot 1) after STEPS_F32 steps.  zeta carries F32 roundoff (~1-3 eps_32), and
 # psi = inverse Laplacian of it amplifies that roundoff in the gravest modes by up to

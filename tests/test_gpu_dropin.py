@@ -184,24 +184,31 @@ def _slot1_equal(b, a):
 
 
 # slot 1 only (slots 2-3 of zeta / psi unmaintained, never read by the reference): after every
-# evolve_zeta! the new zeta is the newest slot qg_slot names, after every step
-# zeta, psi and f_store are what the rotating path holds -- both solvers, F32, the LDS-ring and
-# certifying tendencies (1280 x 1024), HIP-graph replay
+# evolve_zeta! the new zeta is in physical slot 1 (QG_KEEP_ORDER_SLOT1) or in the newest slot
+# qg_slot names (QG_KEEP_ORDER_SLOT1_DEFERRED: slot 2 until the solve's pass A moves it), after
+# every step zeta, psi and f_store are what the rotating path holds, ghost ring included --
+# both solvers, F32, the LDS-ring and certifying tendencies (1280 x 1024), and the pass-A copies
+# of the deferred mode at the benchmarked row lengths: the lane-exchange pass A (M = 4096) and
+# the wide-row pass A (M = 8192, its hand-written ghost-column wrap), F64 and F32
+@pytest.mark.parametrize("deferred", [False, True])
 @pytest.mark.parametrize("M,P,solver,f32", [(64, 48, 0, False), (128, 128, 1, False), (64, 64, 0, True),
-                                            (1280, 1024, 0, False), (1280, 1024, 1, False), (1280, 1024, 0, True)])
-def test_keep_order_slot1_matches_rotation(qg, M, P, solver, f32):
+                                            (1280, 1024, 0, False), (1280, 1024, 1, False), (1280, 1024, 0, True),
+                                            (4096, 16, 0, False), (4096, 16, 0, True), (8192, 8, 0, False),
+                                            (8192, 8, 0, True)])
+def test_keep_order_slot1_matches_rotation(qg, M, P, solver, f32, deferred):
     import torch
-    m = qg.bench_model(M, P=P)
+    m = qg.bench_model(M, P=P, dt=60.0 if M >= 4096 else 30.0 * 60)
     kw = dict(solver=solver, dtype=torch.float32 if f32 else None)
     a = qg.initialise_model(m, **kw)
     b = qg.initialise_model(m, **kw)
-    b.set_keep_order(True, slot1_only=True)
+    b.set_keep_order(True, slot1_only=True, deferred=deferred)
     for t in range(1, 8):
         a.evolve_zeta_(t)
         b.evolve_zeta_(t)
-        # between the calls the newest zeta is where qg_slot says (lean mode, spectral solver:
-        # slot 2 until the solve's pass A moves it into slot 1)
-        assert torch.equal(b.logical("zeta")[0], a.logical("zeta")[0])
+        if deferred:  # the newest zeta is where qg_slot says
+            assert torch.equal(b.logical("zeta")[0], a.logical("zeta")[0])
+        else:  # slot 1 is the newest after every call
+            assert b.heads() == [0, 0, 0] and torch.equal(b.zeta[0], a.logical("zeta")[0])
         a.evolve_psi_()
         b.evolve_psi_()
         assert b.heads() == [0, 0, 0]
@@ -222,21 +229,29 @@ def test_keep_order_slot1_graph_replay(qg, monkeypatch):
     _slot1_equal(st, ref)
 
 
-def test_reference_signatures_slot1(qg):
-    """set_dropin_slots("slot1"): the reference-signature loop on bare arrays, slot 1 of zeta /
-    psi and all of f_store equal to the rotating State after every step."""
+@pytest.mark.parametrize("M,P,mode", [(1280, 1024, "slot1"), (1280, 1024, "slot1_deferred"),
+                                     (256, 128, "slot1"), (256, 128, "slot1_deferred")])
+def test_reference_signatures_slot1(qg, M, P, mode):
+    """set_dropin_slots("slot1" / "slot1_deferred"): the reference-signature loop on bare
+    arrays, slot 1 of zeta / psi and all of f_store equal to the rotating State after every
+    step; with "slot1" also zeta[:, :, :, 1] right after evolve_zeta! -- the contract a caller
+    reading the arrays between the two calls relies on."""
     import torch
-    m = qg.bench_model(1280, P=1024)
+    m = qg.bench_model(M, P=P)
     ref = qg.initialise_model(m)
     zeta, psi, f_store = ref.zeta.clone(), ref.psi.clone(), ref.f_store.clone()
     pc = qg.get_poisson_cholesky(m.M, m.P, m.dx)
     hc = qg.get_helmholtz_cholesky(m.M, m.P, m.dx, qg.S_eig(m))
-    qg.set_dropin_slots("slot1")
+    qg.set_dropin_slots(mode)
     try:
         for t in range(1, 7):
             qg.evolve_zeta_(m, zeta, psi, t, f_store)
+            ref.evolve_zeta_(t)
+            if mode == "slot1":
+                torch.cuda.synchronize()
+                assert torch.equal(zeta[0], _logical(ref)["zeta"][0])
             qg.evolve_psi_(m, zeta, psi, pc, hc)
-            ref.step(t)
+            ref.evolve_psi_()
             la = _logical(ref)
             assert torch.equal(zeta[0], la["zeta"][0]) and torch.equal(psi[0], la["psi"][0])
             assert torch.equal(f_store, la["f_store"])
@@ -263,14 +278,14 @@ def test_keep_order_slot1_to_full_refused(qg):
 
 
 def test_keep_order_slot1_pending_move_settles(qg):
-    """Lean mode, spectral solver: the new zeta waits in slot 2 until the solve; two tendencies
-    in a row, qg_synchronize and qg_canonicalize complete the move into slot 1 first, so every
-    path sees the reference's slot 1."""
+    """Deferred lean mode, spectral solver: the new zeta waits in slot 2 until the solve; two
+    tendencies in a row, qg_synchronize and qg_canonicalize complete the move into slot 1
+    first, so every path sees the reference's slot 1."""
     import torch
     m = qg.bench_model(128)
     a = qg.initialise_model(m)
     b = qg.initialise_model(m)
-    b.set_keep_order(True, slot1_only=True)
+    b.set_keep_order(True, slot1_only=True, deferred=True)
     a.evolve_zeta_(1)
     b.evolve_zeta_(1)
     assert b.heads()[0] == 1  # pending: newest in slot 2

@@ -1,5 +1,5 @@
 """Edge cases of the device path against the C oracle: the smallest grids the spectral solver
-takes (M = 8, P = 2), odd P (chunk of one row), non-square slabs both ways, an explicit chunk
+takes (M = 8, P = 3), the reference's two-point domains (M or P = 2), odd P (chunk of one row), non-square slabs both ways, an explicit chunk
 size, rows of every length up to 262144 points (mixed-radix, split, wide split and Bluestein
 row transforms), and the refusal of what the spectral solver cannot do.  Relative RMS < 1e-10 after a few Euler + AB3 steps."""
 import numpy as np
@@ -43,17 +43,62 @@ def env():
     return qgamd, qg_oracle, qg_ref
 
 
-def test_two_row_domains_are_refused(env):
-    """P_total = 2: the reference's laplacian_1d_periodic (laplacian.jl:41-46) writes the wrap
-    entry over the neighbour entry (both neighbours of a row are the other row), so its matrix is
-    not the periodic 5-point operator its tendency applies -- the device (and the C oracle)
-    would solve the periodic one, 0.28 relative residual against the reference's matrix
-    (r05).  Both solvers refuse such domains (QG_ERR_UNSUPPORTED)."""
+TWO_POINT = [(2, 8), (8, 2), (2, 2), (2, 3), (3, 2), (64, 2), (2, 64), (2, 1001)]
+
+
+def _dev_field(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float64).T)).cuda()
+
+
+@pytest.mark.parametrize("M,P", TWO_POINT)
+def test_two_point_solves_match_reference_matrix(env, M, P):
+    """Global M = 2 or P = 2: the reference's laplacian_1d_periodic (laplacian.jl:40-45) writes
+    its wrap entry over the neighbour entry, so for two points D_2 = [-2 1; 1 -2], not the
+    periodic 5-point operator.  The device's two-point path (spec_twopoint) solves the matrices
+    exactly as construct_spA / get_poisson_cholesky / get_helmholtz_cholesky build them
+    (laplacian.jl:54-75): against splu on those matrices (oracle/qg_ref.py), < 1e-12 relative,
+    the pinned point exactly where the reference puts it."""
+    import torch
     qg, O, R = env
-    for solver in (0, 1):
-        with pytest.raises(qg.QGError) as e:
-            qg.State(qg.bench_model(64, P=2), solver=solver)
-        assert e.value.status == -2, solver
+    dx = 4e6 / max(M, P)
+    alpha = -6.25e-10
+    f = R.update_doubly_periodic_bc(R.seeded_rand(M, P, 7) - 0.5) * 1e-9
+    got = qg.sp_solve_modified_helmholtz(M, P, dx, _dev_field(torch, f), alpha).cpu().numpy().T
+    assert rel(got, R.sp_solve_modified_helmholtz(M, P, dx, f, alpha)) < 1e-12
+    got = qg.sp_solve_poisson(M, P, dx, _dev_field(torch, f)).cpu().numpy().T
+    ref = R.sp_solve_poisson(M, P, dx, f)
+    assert rel(got, ref) < 1e-12
+    assert abs(got[1, 1]) <= 1e-13 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("M,P", TWO_POINT)
+def test_two_point_domains_step_like_the_reference(env, M, P):
+    """The whole loop (run_model_no_output.jl:3-16) on two-point domains against the numpy
+    restatement, whose solves are splu on the reference's own matrices: every slot of zeta and
+    psi < 1e-12 after 6 steps (Euler and AB3).  The C oracle's exact DFT solve would solve the
+    periodic operator, so it is not the reference here.  PCG applies the periodic 5-point
+    stencil and still refuses these domains (QG_ERR_UNSUPPORTED)."""
+    qg, O, R = env
+    steps = 6
+    st = qg.run_model_no_output(qg.bench_model(M, P=P), nsteps=steps)
+    z, p, _ = R.run_model_no_output(R.bench_model(M, P=P), nsteps=steps)
+    for n, ref in (("zeta", z), ("psi", p)):
+        got = st.to_numpy(n)
+        for layer in range(2):
+            assert rel(got[:, :, layer, 0], ref[:, :, layer, 0]) < 1e-12, (n, layer)
+    with pytest.raises(qg.QGError) as e:
+        qg.State(qg.bench_model(M, P=P), solver=1)
+    assert e.value.status == -2
+
+
+def test_two_point_domains_f32(env):
+    """F32 states on a two-point domain: within the F32 bar of the F64 run."""
+    import torch
+    qg, O, R = env
+    m = qg.bench_model(64, P=2)
+    a = qg.run_model_no_output(m, nsteps=4)
+    b = qg.run_model_no_output(m, nsteps=4, dtype=torch.float32)
+    assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 1e-5
 
 
 @pytest.mark.parametrize("M,P,kw", [(8, 3, {}), (16, 48, {}), (64, 16, {}), (16, 128, {}),
@@ -114,7 +159,7 @@ def test_generic_rows_wide(env):
         ref = O.State(R.bench_model(M, P=24, dt=600.0)).run(3)
         assert rel(st.to_numpy("psi"), ref.psi) < TOL, M
     with pytest.raises(qg.QGError) as e:
-        qg.State(qg.bench_model(262145, P=2))
+        qg.State(qg.bench_model(262145, P=4))  # (P = 4: only the row cap can refuse it)
     assert e.value.status == -2
 
 

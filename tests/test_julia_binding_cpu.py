@@ -144,3 +144,23 @@ def test_struct_mirrors_match(cname, jname):
     for (n, ct, cnt), (_, jt) in zip(c, j):
         want = JL_OF_C[ct] if cnt == 0 else f"NTuple{{{cnt},{JL_OF_C[ct]}}}"
         assert jt.replace(" ", "") == want, (cname, n, ct, cnt, jt)
+
+
+def test_dropin_slot_modes_match_the_header():
+    """set_dropin_slots! (Julia) and set_dropin_slots (Python) pass the header's keep-order
+    codes: :slot1 = QG_KEEP_ORDER_SLOT1 (slot 1 newest after every call), :slot1_deferred =
+    QG_KEEP_ORDER_SLOT1_DEFERRED (slot 1 of zeta stale between evolve_zeta! and evolve_psi!),
+    and the Julia docstring states that contract."""
+    hdr = open(HEADER).read()
+    code = {k: int(v) for k, v in re.findall(r"#define (QG_KEEP_ORDER_\w+) (\d+)", hdr)}
+    assert code == {"QG_KEEP_ORDER_SLOT1": 2, "QG_KEEP_ORDER_SLOT1_DEFERRED": 3}
+    text = open(JL).read()
+    m = re.search(r"_DROPIN_SLOTS\[\] = mode === :slot1 \? Cint\((\d)\) : mode === :slot1_deferred \? Cint\((\d)\)",
+                  text)
+    assert m and (int(m.group(1)), int(m.group(2))) == (2, 3)
+    doc = re.search(r'"""`set_dropin_slots!(.*?)"""', text, re.S).group(1)
+    assert "must not be" in doc and "evolve_psi!" in doc
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "julia-ocean-modelling_amd"))
+    from qgamd import _lib
+    assert (_lib.QG_KEEP_ORDER_SLOT1, _lib.QG_KEEP_ORDER_SLOT1_DEFERRED) == (2, 3)

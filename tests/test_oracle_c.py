@@ -117,3 +117,32 @@ def test_wind_forcing_extension_term():
     np.testing.assert_allclose(d, np.broadcast_to(w, d.shape), rtol=0, atol=1e-14 * np.abs(w).max() + 4e-16 * scale)
     assert np.array_equal(b.f_store[:, :, 1, 0], a.f_store[:, :, 1, 0])
     assert np.abs(w).max() > 0
+
+
+@pytest.mark.parametrize("M,P,alpha,pinned", [(16, 16, 0.0, True), (12, 20, 0.0, True), (32, 16, -6.25e-10, False),
+                                              (9, 30, -1e-10, False)])
+def test_longdouble_solve_matches_sparse_direct(M, P, alpha, pinned):
+    """The extended-precision solve (qg_ref.solve_longdouble) solves the reference's own
+    matrices (splu on construct_spA / get_poisson_cholesky): agreement to F64 roundoff."""
+    dx = 4e6 / M
+    f = _rand(M, P, 9) * 1e-9
+    got = np.asarray(R.solve_longdouble(M, P, dx, alpha, f, pinned=pinned), dtype=np.float64)
+    ref = R.sp_solve_poisson(M, P, dx, f) if pinned else R.sp_solve_modified_helmholtz(M, P, dx, f, alpha)
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 1e-12
+
+
+@pytest.mark.parametrize("M,P", [(64, 16384), (256, 8192), (512, 512)])
+def test_c_oracle_solve_against_longdouble_on_long_grids(M, P):
+    """The C oracle's DFT solve against the long-double solve on long domains, where the
+    pinned Poisson problem's gravest modes have eigenvalues ~ (2 pi / P)^2: relative error
+    < 1e-11 (measured 1.0e-12 at 64 x 16384).  Round 6 replaced its eigenvalue expression
+    2 cos(t) + 2 cos(s) - 4 by -4 (sin^2(t/2) + sin^2(s/2)): the old form lost those
+    eigenvalues to cancellation (7.5e-10 at 64 x 16384, 2.0e-9 at 256 x 32768), which was the
+    larger part of the device-vs-oracle differences on long grids."""
+    dx = 4e6 / M
+    f = _rand(M, P, 17) * 1e-9
+    for alpha, pinned in ((0.0, True), (-6.25e-10, False)):
+        x = R.solve_longdouble(M, P, dx, alpha, f, pinned=pinned)
+        got = O.solve(M, P, dx, alpha, f, pinned=pinned)
+        e = float(np.linalg.norm((got - x)[1:-1, 1:-1]) / np.linalg.norm(x[1:-1, 1:-1]))
+        assert e < 1e-11, (M, P, pinned, e)
