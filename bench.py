@@ -582,6 +582,11 @@ def main():
         # (under torch.distributed.run: the probe group first, from this rank's own child)
         extra = torchrun_probe(args, sys.argv[1:])
         args = parse(sys.argv[1:] + extra)
+    if args.probe_peer and os.environ.get("QG_BENCH_PROBE_KILL") == os.environ.get("RANK"):
+        # (rehearsal of the fallback: this probe rank dies as a fault in the cross-device path
+        # would kill it, before it touches the GPU)
+        import signal
+        os.kill(os.getpid(), signal.SIGSEGV)
     if args.graph:
         os.environ["QG_GRAPH"] = "1"
     one_gpu = args.one_gpu and args.gpus > 1 and args.transport == "rccl"

@@ -279,25 +279,26 @@ def test_bluestein_rows_pcg(env, M, P):
 
 
 def test_bluestein_rows_f32(env):
-    """F32 state through the Bluestein rows (M = 20000): psi within the white-noise F32 bar."""
+    """F32 state through the Bluestein rows (M = 20000): F32 vs F64 within the mechanism's
+    derived bars (tests/f32_model.py: zeta at F32 roundoff, psi = the solve's image of it)."""
     import torch
+    import f32_model as F32
     qg, O, R = env
-    m = qg.bench_model(20000, P=4, dt=60.0)
-    a = qg.run_model_no_output(m, nsteps=2)
-    b = qg.run_model_no_output(m, nsteps=2, dtype=torch.float32)
-    assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 2e-2
+    r = F32.decompose(qg, torch, qg.bench_model(20000, P=4, dt=60.0), 2, mc=8)
+    print(F32.fmt(r))
+    F32.check(r)
 
 
 def test_wide_split_rows_f32(env):
-    """F32 state through the wide split (M = 16384): psi within the white-noise F32 bar of
-    DESIGN.md section 4 (2e-2: psi = A^-1 zeta amplifies zeta's F32 rounding in the gravest
-    modes by up to (M / 2 pi)^2; measured 1.0e-2 here)."""
+    """F32 state through the wide split (M = 16384): F32 vs F64 within the mechanism's derived
+    bars (tests/f32_model.py; psi = A^-1 zeta amplifies zeta's F32 rounding in the gravest modes
+    by up to (M / 2 pi)^2; measured 1.0e-2 here in r05)."""
     import torch
+    import f32_model as F32
     qg, O, R = env
-    m = qg.bench_model(16384, P=32, dt=60.0)
-    a = qg.run_model_no_output(m, nsteps=3)
-    b = qg.run_model_no_output(m, nsteps=3, dtype=torch.float32)
-    assert rel(b.to_numpy("psi").astype(np.float64), a.to_numpy("psi")) < 2e-2
+    r = F32.decompose(qg, torch, qg.bench_model(16384, P=32, dt=60.0), 3, mc=8)
+    print(F32.fmt(r))
+    F32.check(r)
 
 
 def test_invalid_arguments_are_refused(env):

@@ -211,10 +211,10 @@ def _config_worker(rank, world, port, M, steps, outdir, f32):
     dist.destroy_process_group()
 
 
-# bars: test_gpu_configs.py's (F32 psi: the white-noise field's rounding amplified by the
-# gravest Poisson modes)
+# bars: test_gpu_configs.py's (F32: zeta < 16 eps_32, psi by the mechanism's derived bars of
+# tests/f32_model.py -- the white-noise field's rounding amplified by the gravest Poisson modes)
 @pytest.mark.parametrize("world,M,steps,f32,tol", [(4, 4096, 4, False, {"zeta": 1e-10, "psi": 1e-10}),
-                                                   (8, 8192, 3, True, {"zeta": 1e-6, "psi": 1e-2})])
+                                                   (8, 8192, 3, True, {"zeta": 16 * 2.0 ** -24, "psi": 1.0})])
 def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, capsys):
     """config 4: four 4096^2 F64 slabs (global 4096 x 16384); config 5: eight 8192^2 F32 slabs
     (global 8192 x 65536) -- over multi-rank RCCL, against the single-GPU run of the global
@@ -251,9 +251,25 @@ def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, capsys):
                 a = torch.from_numpy(np.load(os.path.join(d, f"{n}{r}.npy"))).cuda().double()
                 e = float(torch.linalg.vector_norm((a - g).reshape(-1)) / torch.linalg.vector_norm(g.reshape(-1)))
                 worst[n] = max(worst.get(n, 0.0), e)
+        rec = None
+        if f32:
+            import f32_model as F32
+            asm = {}
+            for n in ("zeta", "psi"):
+                full = torch.zeros((2, world * M + 2, M + 2), dtype=torch.float32, device="cuda")
+                for r in range(world):
+                    a = torch.from_numpy(np.load(os.path.join(d, f"{n}{r}.npy"))).cuda()
+                    full[:, 1 + r * M: 1 + (r + 1) * M] = a[:, 1:M + 1]
+                asm[n] = full
+            rec = F32.compare(qgamd, torch, m, [asm["zeta"][0], asm["zeta"][1]], [asm["psi"][0], asm["psi"][1]],
+                              [glob.current("zeta", 1), glob.current("zeta", 2)],
+                              [glob.current("psi", 1), glob.current("psi", 2)], mc=8)
     with capsys.disabled():
-        print(f"\nRCCL {world} x {M}^2 {'F32' if f32 else 'F64'} slabs vs one GPU, {steps} steps: {worst}")
+        print(f"\nRCCL {world} x {M}^2 {'F32' if f32 else 'F64'} slabs vs one GPU, {steps} steps: {worst}"
+              + (f"; {F32.fmt(rec)}; bars {F32.bars(rec)}" if rec else ""))
     assert all(worst[n] < tol[n] for n in worst), worst
+    if rec:
+        F32.check(rec)
 
 
 # ---- failure paths over multi-rank RCCL -------------------------------------------------

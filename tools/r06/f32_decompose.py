@@ -16,15 +16,11 @@ def main():
     m = qgamd.bench_model(M, P=P, dt=60.0)
     r = decompose(qgamd, torch, m, steps, mc)
     for k, v in r.items():
-        if k == "pred_draws":
-            continue
         if isinstance(v, list):
             v = "[" + ", ".join(f"{x:.3e}" for x in v) + "]"
         elif isinstance(v, float):
             v = f"{v:.3e}"
         print(f"{k:16s} {v}")
-    print("pred draws (max over draws per part):",
-          ["%.3e" % max(d[i] for d in r["pred_draws"]) for i in range(3)])
     print(f"eps32 = {EPS32:.3e}; psi_err / eps32 = {r['psi_err'] / EPS32:.1f}, "
           f"e_solve / eps32 = {r['e_solve'] / EPS32:.1f}, zeta_err / eps32 = {r['zeta_err'] / EPS32:.1f}")
 
