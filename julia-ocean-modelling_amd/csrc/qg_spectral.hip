@@ -1733,6 +1733,12 @@ constexpr int SPL_T = 512;        // row-transform threads (256 VGPRs: a radix-1
 constexpr int SPL_MMAX = 8192;    // one LDS buffer of M complex (128 KB)
 constexpr int SPL_WMAX = 2 * SPL_MMAX;  // even rows up to here: one system at a time, half length
 constexpr int SPL_KT = 256;       // recurrence kernels: wavenumbers per workgroup
+// SPL_U_F64: the split pipeline keeps U in F64 for F32 states too.  Its U holds the raw row
+// spectra F (and then u, X) between kernels; rounding F to F32 is a second F32 rounding of
+// zeta~ whose gravest modes the solve amplifies by up to (L / 2 pi)^2 / dx^2 -- measured
+// (r06, tools/r06/f32_solve_err.py): the F32 state's solve vs the F64 solve of the same zeta
+// 3.4e-4 (5000 x 32), 6.1e-4 (16384 x 32), 4.1e-3 (20000 x 4: 69 000 eps_32), against
+// 0.7 eps_32 in the fused passes, which store only the filtered u (no amplification).
 
 // One decimation-in-frequency stage of radix R, in place: butterfly (block b, n) reads the R
 // values n + m span of its block, does the R-point DFT, multiplies output q by W_Ls^(n q)
@@ -1834,7 +1840,7 @@ __device__ void spl_fft(double2 *buf, const SpecArgs &a, const double2 *tw, int 
 
 template <class S, bool INV>
 __global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
-    using US = typename Store<S>::C;
+    using US = double2;  // (F64 whatever the state: see SPL_U_F64)
     const int M = (int)a.M, NH = M / 2, t = threadIdx.x;
     const bool odd = M & 1;
     const int KC = odd ? NH + 1 : NH;  // (see spec_passA_gen)
@@ -1864,17 +1870,17 @@ __global__ __launch_bounds__(SPL_T) void spec_fft_split(SpecArgs a) {
             for (int k = t; k < KC; k += SPL_T) {
                 const double2 Zk = Z(k);
                 if (k == 0) {  // real lines k = 0 (and k = M/2 for even M)
-                    Urow[0] = Store<S>::c(make_double2(Zk.x, 0));
-                    Urow[KS] = Store<S>::c(make_double2(Zk.y, 0));
+                    Urow[0] = Store<double>::c(make_double2(Zk.x, 0));
+                    Urow[KS] = Store<double>::c(make_double2(Zk.y, 0));
                     if (!odd) {
                         const double2 Zn = Z(NH);
-                        Urow[NH] = Store<S>::c(make_double2(Zn.x, 0));
-                        Urow[KS + NH] = Store<S>::c(make_double2(Zn.y, 0));
+                        Urow[NH] = Store<double>::c(make_double2(Zn.x, 0));
+                        Urow[KS + NH] = Store<double>::c(make_double2(Zn.y, 0));
                     }
                 } else {
                     const double2 Zm = Z(M - k);
-                    Urow[k] = Store<S>::c(make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5));
-                    Urow[KS + k] = Store<S>::c(make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5));
+                    Urow[k] = Store<double>::c(make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5));
+                    Urow[KS + k] = Store<double>::c(make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5));
                 }
             }
             __syncthreads();  // the next row overwrites buf
@@ -1928,7 +1934,7 @@ static_assert(!WPlan::PINGPONG && !FftPlan<SPL_MMAX, WIDE_FT>::PINGPONG, "the 81
 static_assert(FftPlan<SPL_MMAX, WIDE_FT>::LDS == WPlan::LDS, "one LDS size for both directions");
 template <class S, bool INV, bool POW2, int WT = POW2 ? (INV ? WIDE_T : WIDE_FT) : SPL_T>
 __global__ __launch_bounds__(WT) void spec_fft_wide(SpecArgs a) {
-    using US = typename Store<S>::C;
+    using US = double2;  // (F64 whatever the state: see SPL_U_F64)
     const int M = POW2 ? 2 * SPL_MMAX : (int)a.M, H = M / 2, t = threadIdx.x;
     const int KS = a.KS;
     const int64_t Pl = a.P, ld = a.ld;
@@ -2002,13 +2008,13 @@ __global__ __launch_bounds__(WT) void spec_fft_wide(SpecArgs a) {
                 for (int k = t; k < H; k += WT) {
                     const double2 Zk = Zat(k);
                     if (k == 0) {  // X_0 = Re + Im, X_H = Re - Im (both real)
-                        Us[0] = Store<S>::c(make_double2(Zk.x + Zk.y, 0));
-                        Us[H] = Store<S>::c(make_double2(Zk.x - Zk.y, 0));
+                        Us[0] = Store<double>::c(make_double2(Zk.x + Zk.y, 0));
+                        Us[H] = Store<double>::c(make_double2(Zk.x - Zk.y, 0));
                     } else {
                         const double2 Zm = Zat(H - k);
                         const double2 E = make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5);
                         const double2 O = make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5);
-                        Us[k] = Store<S>::c(cadd(E, cmul(twM[k], O)));
+                        Us[k] = Store<double>::c(cadd(E, cmul(twM[k], O)));
                     }
                 }
                 __syncthreads();  // the next transform overwrites buf
@@ -2075,7 +2081,7 @@ __global__ __launch_bounds__(WT) void spec_fft_wide(SpecArgs a) {
 // lines k of (chunk blockIdx.x): the generic pass A's backward filter and summaries
 template <class S>
 __global__ __launch_bounds__(SPL_KT) void spec_passA_split(SpecArgs a) {
-    using US = typename Store<S>::C;
+    using US = double2;  // (F64 whatever the state: see SPL_U_F64)
     const int c = blockIdx.x, k = blockIdx.y * SPL_KT + threadIdx.x;
     if (k >= a.KH) return;
     const int KS = a.KS, s0 = c * a.L, e = s0 + a.L - 1;
@@ -2098,7 +2104,7 @@ __global__ __launch_bounds__(SPL_KT) void spec_passA_split(SpecArgs a) {
                 a.hline[j] = B.x;
             }
             u[s] = cfma(rr[s].x, u[s], cscale(B, cs[s]));
-            Urow[s * KS + k] = Store<S>::c(u[s]);
+            Urow[s * KS + k] = Store<double>::c(u[s]);
             bw[s] = cfma(rr[s].y, bw[s], u[s]);
         }
     }
@@ -2114,7 +2120,7 @@ __global__ __launch_bounds__(SPL_KT) void spec_passA_split(SpecArgs a) {
 // lines k of (chunk blockIdx.x): carries, the generic pass B's forward filter, X in place
 template <class S>
 __global__ __launch_bounds__(SPL_KT) void spec_passB_split(SpecArgs a) {
-    using US = typename Store<S>::C;
+    using US = double2;  // (F64 whatever the state: see SPL_U_F64)
     const int c = blockIdx.x, k = blockIdx.y * SPL_KT + threadIdx.x;
     if (k >= a.KH) return;
     const int KS = a.KS, L = a.L, s0 = c * L, e = s0 + L - 1;
@@ -2140,7 +2146,7 @@ __global__ __launch_bounds__(SPL_KT) void spec_passB_split(SpecArgs a) {
             w[s] = cfma(rr[s].x, w[s], cadd(ul, cu[s]));
             cu[s] = cscale(cu[s], rr[s].y);
             const double2 X = (s == 0 && sing) ? make_double2((line0 + (double)j * line1) + a.line[j], 0) : w[s];
-            Urow[s * KS + k] = Store<S>::c(X);
+            Urow[s * KS + k] = Store<double>::c(X);
         }
     }
 }
@@ -2220,7 +2226,7 @@ __global__ __launch_bounds__(BL_T) void bl_load_fwd(SpecArgs a, int64_t r0, int 
 // Z_k = c_k Y_k, split into the two systems' spectra B_s(k) in U (spec_fft_split's forward)
 template <class S>
 __global__ __launch_bounds__(BL_T) void bl_store_fwd(SpecArgs a, int64_t r0, int rows, const double2 *Y) {
-    using US = typename Store<S>::C;
+    using US = double2;  // (F64 whatever the state: see SPL_U_F64)
     const int M = (int)a.M, NH = M / 2, L = a.bl_L, KS = a.KS;
     const bool odd = M & 1;
     const int KC = odd ? NH + 1 : NH;
@@ -2233,17 +2239,17 @@ __global__ __launch_bounds__(BL_T) void bl_store_fwd(SpecArgs a, int64_t r0, int
         auto Z = [&](int q) { return cmul(a.bl_chirp[q], y[q]); };
         const double2 Zk = Z(k);
         if (k == 0) {  // real lines k = 0 (and k = M/2 for even M)
-            Urow[0] = Store<S>::c(make_double2(Zk.x, 0));
-            Urow[KS] = Store<S>::c(make_double2(Zk.y, 0));
+            Urow[0] = Store<double>::c(make_double2(Zk.x, 0));
+            Urow[KS] = Store<double>::c(make_double2(Zk.y, 0));
             if (!odd) {
                 const double2 Zn = Z(NH);
-                Urow[NH] = Store<S>::c(make_double2(Zn.x, 0));
-                Urow[KS + NH] = Store<S>::c(make_double2(Zn.y, 0));
+                Urow[NH] = Store<double>::c(make_double2(Zn.x, 0));
+                Urow[KS + NH] = Store<double>::c(make_double2(Zn.y, 0));
             }
         } else {
             const double2 Zm = Z(M - k);
-            Urow[k] = Store<S>::c(make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5));
-            Urow[KS + k] = Store<S>::c(make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5));
+            Urow[k] = Store<double>::c(make_double2((Zk.x + Zm.x) * 0.5, (Zk.y - Zm.y) * 0.5));
+            Urow[KS + k] = Store<double>::c(make_double2((Zk.y + Zm.y) * 0.5, (Zm.x - Zk.x) * 0.5));
         }
     }
 }
@@ -2252,7 +2258,7 @@ __global__ __launch_bounds__(BL_T) void bl_store_fwd(SpecArgs a, int64_t r0, int
 // A_n = conj(Z_n) c_n, 0 beyond M
 template <class S>
 __global__ __launch_bounds__(BL_T) void bl_load_inv(SpecArgs a, int64_t r0, int rows, double2 *A) {
-    using US = typename Store<S>::C;
+    using US = double2;  // (F64 whatever the state: see SPL_U_F64)
     const int M = (int)a.M, NH = M / 2, L = a.bl_L, KS = a.KS;
     const bool odd = M & 1;
     const int KC = odd ? NH + 1 : NH;
