@@ -582,6 +582,12 @@ def main():
         # (under torch.distributed.run: the probe group first, from this rank's own child)
         extra = torchrun_probe(args, sys.argv[1:])
         args = parse(sys.argv[1:] + extra)
+    # this process's stdout (fd 1) carries the JSON line alone: whatever the libraries write
+    # there -- RCCL's version banner at communicator set-up, a rocprofv3 child's notes -- goes to
+    # stderr until the line is printed (the driver reads the line from stdout)
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     if args.probe_peer and os.environ.get("QG_BENCH_PROBE_KILL") == os.environ.get("RANK"):
         # (rehearsal of the fallback: this probe rank dies as a fault in the cross-device path
         # would kill it, before it touches the GPU)
@@ -965,6 +971,8 @@ def main():
     else:
         out["cpu_baseline"] = None
     validate_record(out)
+    sys.stdout.flush()
+    os.dup2(json_fd, 1)
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
