@@ -6,6 +6,10 @@ MI355X, with the HBM roofline of the dominant kernel and the CPU oracle timed be
 N > 1 runs one process per GPU: under torch.distributed.run (RANK / WORLD_SIZE from the
 environment), or, launched plainly with WORLD_SIZE unset, bench.py starts the N rank
 processes itself (spawn_ranks; the parent never touches the GPU) and passes rank 0's line on.
+Before the bench ranks, a probe group of N separate rank processes tries the peer transports
+(the default data path) at 256^2 per GPU; only if every probe rank exits 0 do the bench ranks
+use them, else RCCL (config.transport_probe says why; --no-probe skips it).  Each rank's
+stdout carries the JSON line alone (library output goes to stderr).
 
 Workload (BASELINE.json configs[2]; per GPU for N > 1, slabs in y, weak scaling):
   2-layer Phillips, N x N interior per GPU, Float64, bench parameters of
