@@ -123,6 +123,9 @@ def parse(argv=None):
                          "halo overlap toggled (overlap_ab)")
     ap.add_argument("--comm-self", action="store_true",
                     help="single GPU through the multi-GPU path (1-rank RCCL ring): measures its overhead")
+    ap.add_argument("--no-reference-runs", dest="reference_runs", action="store_false", default=True,
+                    help="N = 1: skip re-running the reference's own benchmark configuration (M = 8 ... 256, "
+                         "24 steps of dt = 60 min) beside its published Julia times (reference_benchmark)")
     ap.add_argument("--no-probe", dest="probe", action="store_false", default=True,
                     help="N > 1 over RCCL: skip the peer-transport probe group (below) and let the ranks "
                          "choose the transports themselves")
@@ -174,7 +177,7 @@ def pmc_live(args, timeout_s=150):
              "--dt", str(args.dt), "--chunk-rows", str(args.chunk_rows), "--steps", "5", "--warmup", "3",
              "--clock-warm-ms", "0",
              "--cpu-steps", "0", "--cpu-steps-1t", "0", "--pcg-steps", "0", "--dropin-steps", "0",
-             "--no-pmc-live"]
+             "--no-pmc-live", "--no-reference-runs"]
     vals = {}
     try:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -305,6 +308,39 @@ def cpu_baseline(n, dt, steps, threads, steps_1t):
         out["single_thread"] = {"value": steps_1t / el1, "unit": "timesteps/s", "cores": 1,
                                 "sample": f"{steps_1t} AB3 timestep(s), same model, 1 thread, {el1:.2f} s wall"}
     return out
+
+
+# The reference's own benchmark (src/benchmarking/benchmarking.jl:6-41): the minimum wall time
+# (@belapsed) of the whole run_model_no_output -- initialisation, the two factorisations, 24
+# steps of dt = 60 min (T = 1 day) -- at M = P; its published Julia times, unstated CPU
+# (notebooks/jupyter/julia_parts_graph.ipynb:125).
+REFERENCE_JULIA_S = {8: 6.553e-3, 16: 14.737e-3, 32: 66.247e-3, 64: 247.989e-3, 128: 1.070, 256: 5.141}
+
+
+def reference_benchmark(qgamd, torch, samples=5):
+    """The same measurement of this implementation on the GPU: context set-up (the solver's
+    tables replace the factorisations), seeded initialisation, the 24 steps and the slots put
+    back in the reference's order (qg_canonicalize), synchronised; the minimum over `samples`
+    runs after one warm run, next to the reference's published time."""
+    rows = []
+    for M, ref_s in REFERENCE_JULIA_S.items():
+        m = qgamd.bench_model(M, dt=3600.0)
+        best = float("inf")
+        for k in range(samples + 1):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            st = qgamd.run_model_no_output(m)
+            st.canonicalize()
+            st.synchronize()
+            el = time.perf_counter() - t0
+            st.close()
+            if k > 0:
+                best = min(best, el)
+        rows.append({"M": M, "steps": int(m.T // m.dt), "gpu_s": best, "reference_julia_s": ref_s,
+                     "speedup": ref_s / best})
+    return {"runs": rows, "note": "the reference's own benchmark (benchmarking.jl: run_model_no_output, dt = 60 min, "
+                                  "T = 1 day, M = P, minimum over samples) against its published Julia times "
+                                  "(julia_parts_graph.ipynb:125; unstated CPU, 1 core per scripts/benchmarking_job.sh)"}
 
 
 def pcg_variant(qgamd, m, n, warmup, K, torch, warm_ms=300.0):
@@ -970,6 +1006,11 @@ def main():
             except Exception as e:  # noqa: BLE001 -- reported, the headline line is still printed
                 d = {"error": f"{type(e).__name__}: {e}"}
             out[key] = d
+    if args.reference_runs and world == 1 and not args.comm_self:
+        try:
+            out["reference_benchmark"] = reference_benchmark(qgamd, torch)
+        except Exception as e:  # noqa: BLE001 -- reported, the headline line is still printed
+            out["reference_benchmark"] = {"error": f"{type(e).__name__}: {e}"}
     if args.cpu_steps > 0 and world == 1 and args.dtype == "f64":
         out["cpu_baseline"] = cpu_baseline(n, args.dt, args.cpu_steps, args.cpu_threads, args.cpu_steps_1t)
     else:

@@ -64,3 +64,43 @@ def test_verify_peer_falls_back_on_one_ulp():
     why = bench.verify_peer(st, torch, None, sync=lambda: None, device="cpu")
     assert why is not None and "differed" in why
     assert (st.halo_transport, st.gather_transport) == ("rccl", "rccl")
+
+
+def test_reference_benchmark_configuration():
+    """reference_benchmark re-runs the reference's own benchmark configuration
+    (benchmarking.jl: dt = 60 min, T = 1 day -> 24 steps, M = P = 8 ... 256) and sets the
+    minimum over samples beside the published Julia times (julia_parts_graph.ipynb:125)."""
+    seen = []
+
+    class St:
+        def canonicalize(self):
+            seen.append("canon")
+
+        def synchronize(self):
+            pass
+
+        def close(self):
+            pass
+
+    class Q:
+        @staticmethod
+        def bench_model(M, dt):
+            from types import SimpleNamespace
+            return SimpleNamespace(M=M, P=M, dt=dt, T=86400.0)
+
+        @staticmethod
+        def run_model_no_output(m):
+            seen.append((m.M, m.dt))
+            return St()
+
+    class T:
+        class cuda:
+            @staticmethod
+            def synchronize():
+                pass
+
+    r = bench.reference_benchmark(Q, T, samples=2)
+    assert [x["M"] for x in r["runs"]] == [8, 16, 32, 64, 128, 256]
+    assert all(x["steps"] == 24 and x["reference_julia_s"] == bench.REFERENCE_JULIA_S[x["M"]] for x in r["runs"])
+    assert all(x["speedup"] == x["reference_julia_s"] / x["gpu_s"] for x in r["runs"])
+    assert seen.count("canon") == 6 * 3 and (256, 3600.0) in seen

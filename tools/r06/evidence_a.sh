@@ -23,7 +23,7 @@ for f in ["$O/bench_driver_%d.json" % k for k in (1, 2, 3)] + ["$O/bench_default
           "; cpu", round(d["cpu_baseline"]["value"], 3), d["cpu_baseline"]["cores"])
 PY
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o drv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc-live --cpu-steps 0 > $R/$O/prof.log 2>&1 || exit 4
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o drv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc-live --no-reference-runs --cpu-steps 0 > $R/$O/prof.log 2>&1 || exit 4
 cut -d, -f1-4 $R/$O/prof/drv_kernel_stats.csv | head -8 | tee -a $R/$O/summary.txt
 cd $R && bash tools/pmc.sh ev_$TAG > $O/pmc.log 2>&1 || exit 5
 echo done | tee -a $O/summary.txt
