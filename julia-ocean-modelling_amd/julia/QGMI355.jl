@@ -146,7 +146,8 @@ evolve_psi!(model, s::QGState, poisson=nothing, helmholtz=nothing) =
 # A caller that keeps the reference's own loop (`evolve_zeta!(model, zeta, psi, t, f_store)`
 # then `evolve_psi!(model, zeta, psi, P, H)`) on device arrays gets a library context bound to
 # those arrays, created on first use and cached by the arrays' addresses.  Each call leaves
-# the arrays in the reference's slot order (slot 1 = newest), as store_new_state! does, so
+# the arrays in the reference's slot order (slot 1 = newest), as store_new_state! does (with
+# `set_dropin_slots!(:slot1_deferred)` zeta's slot 1 only after evolve_psi!, see there), so
 # `zeta[:, :, 1, 1]` means what it means in the reference: the context keeps that order on
 # the device (qg_set_keep_order: the history shifted in place before each new value, two
 # slot copies per field, the reference's own data movement).  (The rotation-free fast path
