@@ -2488,8 +2488,8 @@ static int dispatch_pass(bool passB, const SpecArgs &a, hipStream_t s) {
 // of point 1 -> identity, b[1] = 0; laplacian.jl:66-75, model.jl:185) is the unpinned solution y
 // plus the multiple of z = A0^-1 e_1 that zeroes point 1: x = y - (y_1 / z_1) z (only the first
 // equation is dropped, so A x = b + mu e_1 with x_1 = 0).  z is solved once at init by the same
-// kernel (unit = 1).  One workgroup: four threads run the lines, then all threads combine the
-// modes, pin, back-project and write the ghost ring.  No performance at stake (a test domain).
+// kernel (unit = 1).  One workgroup: all threads stage the right-hand sides, four threads run the
+// lines, then all threads combine the modes, pin, back-project and write the ghost ring.  No performance at stake (a test domain).
 template <class S>
 __global__ __launch_bounds__(256) void spec_twopoint(SpecArgs a, int unit) {
     const int64_t M = a.M, P = a.P, ld = a.ld, N = a.two_N;
@@ -2499,36 +2499,48 @@ __global__ __launch_bounds__(256) void spec_twopoint(SpecArgs a, int unit) {
         return a.two_yline ? fidx(1 + t, n + 1, ld) : fidx(n + 1, 1 + t, ld);
     };
     const S *in1 = static_cast<const S *>(a.in1), *in2 = static_cast<const S *>(a.in2);
-    if (threadIdx.x < 4) {
+    // the four right-hand sides, staged by the whole workgroup (coalesced): line (s, q) gets
+    // dx^2 (zeta~_a +- zeta~_b) of mode q; unit: -dx^2 e_1 in both modes of system 0
+    for (int64_t e = threadIdx.x; e < 4 * N; e += blockDim.x) {
+        const int sq = (int)(e / N), s = sq >> 1, q = sq & 1;
+        const int64_t n = e - (int64_t)sq * N;
+        double v = 0.0;
+        if (unit) {
+            v = n == 0 ? -dx2 : 0.0;
+        } else {
+            const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];
+            const int64_t o0 = idx(n, 0), o1 = idx(n, 1);
+            // b[1] = 0: system 0's pinned point drops out of its right-hand side
+            const double v0 = (s == 0 && a.pinned0 && n == 0) ? 0.0 : pa * (double)in1[o0] + pb * (double)in2[o0];
+            const double v1 = pa * (double)in1[o1] + pb * (double)in2[o1];
+            v = dx2 * (q == 0 ? v0 + v1 : v0 - v1);
+        }
+        a.two_X[e] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {  // the line solves, in place over the staged right-hand sides
         const int s = threadIdx.x >> 1, q = threadIdx.x & 1;
         double *X = a.two_X + (size_t)(2 * s + q) * N;
         if (!unit || s == 0) {
-            const double pa = a.pin_in[2 * s], pb = a.pin_in[2 * s + 1];
-            auto zt = [&](int64_t n, int t) -> double {
-                if (s == 0 && a.pinned0 && n == 0 && t == 0) return 0.0;  // b[1] = 0
-                const int64_t o = idx(n, t);
-                return pa * (double)in1[o] + pb * (double)in2[o];
-            };
-            // right-hand side of mode q: dx^2 (zeta~_a +- zeta~_b); unit: -dx^2 e_1 in both modes
-            auto R = [&](int64_t n) -> double {
-                if (unit) return n == 0 ? -dx2 : 0.0;
-                const double v0 = zt(n, 0), v1 = zt(n, 1);
-                return dx2 * (q == 0 ? v0 + v1 : v0 - v1);
-            };
             const double r = a.two_r[s][q];
             if (N == 2) {  // [a 1; 1 a]^-1 = [a -1; -1 a] / (a^2 - 1), a = two_r
-                const double r0 = R(0), r1 = R(1), den = r * r - 1.0;
+                const double r0 = X[0], r1 = X[1], den = r * r - 1.0;
                 X[0] = (r * r0 - r1) / den;
                 X[1] = (r * r1 - r0) / den;
             } else {
                 // w = (1 - r S-)^-1 R: w_n = R_n + r w_{n-1}, w_0 = sum_m r^m R_{-m} / (1 - r^N)
                 double acc = 0.0, pw = 1.0;
                 for (int64_t m = 0; m < N && pw != 0.0; ++m) {
-                    acc += pw * R((N - m) % N);
+                    acc += pw * X[(N - m) % N];
                     pw *= r;
                 }
-                X[0] = acc * a.two_inv1mrN[s][q];
-                for (int64_t n = 1; n < N; ++n) X[n] = R(n) + r * X[n - 1];
+                double w = acc * a.two_inv1mrN[s][q];
+                X[0] = w;
+#pragma unroll 8
+                for (int64_t n = 1; n < N; ++n) {
+                    w = X[n] + r * w;
+                    X[n] = w;
+                }
                 // v = (1 - r S+)^-1 w: v_n = w_n + r v_{n+1}, v_{N-1} = sum_m r^m w_{N-1+m} / (1 - r^N)
                 acc = 0.0;
                 pw = 1.0;
@@ -2538,6 +2550,7 @@ __global__ __launch_bounds__(256) void spec_twopoint(SpecArgs a, int unit) {
                 }
                 double v = acc * a.two_inv1mrN[s][q];
                 X[N - 1] = -r * v;
+#pragma unroll 8
                 for (int64_t n = N - 2; n >= 0; --n) {
                     v = X[n] + r * v;
                     X[n] = -r * v;

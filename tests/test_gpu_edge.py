@@ -50,7 +50,7 @@ def _dev_field(torch, a):
     return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float64).T)).cuda()
 
 
-@pytest.mark.parametrize("M,P", TWO_POINT)
+@pytest.mark.parametrize("M,P", TWO_POINT + [(2, 20000), (20000, 2)])
 def test_two_point_solves_match_reference_matrix(env, M, P):
     """Global M = 2 or P = 2: the reference's laplacian_1d_periodic (laplacian.jl:40-45) writes
     its wrap entry over the neighbour entry, so for two points D_2 = [-2 1; 1 -2], not the
