@@ -36,7 +36,7 @@ def _rel(torch, a, b):
     return float(d / torch.linalg.vector_norm(b.double().reshape(-1)))
 
 
-def _run_slabs(torch, qgamd, ThreadRing, m, G, steps, dtype, init=None):
+def _run_slabs(torch, qgamd, ThreadRing, m, G, steps, dtype, init=None, solver=0):
     """G slab States of model m (P = G * P_local) stepped through the ThreadRing transport.
     init(r, st): called after each slab's qg_initialise (e.g. to overwrite its slot 0)."""
     Pl = m.P // G
@@ -45,7 +45,7 @@ def _run_slabs(torch, qgamd, ThreadRing, m, G, steps, dtype, init=None):
     for r in range(G):
         s = torch.cuda.Stream()
         with torch.cuda.stream(s):
-            st = qgamd.State(m, P_local=Pl, dtype=dtype)
+            st = qgamd.State(m, P_local=Pl, dtype=dtype, solver=solver)
         ring.attach(st, r)
         ranks.append((st, s))
 
@@ -97,6 +97,27 @@ def test_config4_four_4096_slabs(env, capsys):
     worst = _compare_slabs(torch, glob, slabs, 1e-10)
     with capsys.disabled():
         print(f"\nconfig 4 (4 x 4096^2 F64 slabs vs one GPU, {steps} steps): worst rel diff {worst}")
+
+
+def test_config4_pcg_slabs(env, capsys):
+    """BASELINE config 4 with the north star's solver form: four 4096^2 F64 slabs whose
+    evolve_psi! is the matrix-free PCG on the 5-point stencil (spectral preconditioner, the
+    rank sums of its dot products gathered across the slabs, every solve certified on the
+    device), against one GPU's direct solve of the global grid: every slot < 1e-10, and every
+    slab's certificate record shows each solve certified, none failed."""
+    torch, qgamd, ThreadRing = env
+    G, N, steps = 4, 4096, 4
+    m = qgamd.bench_model(N, P=G * N, dt=60.0)
+    glob = qgamd.run_model_no_output(m, nsteps=steps)
+    torch.cuda.synchronize()
+    slabs = _run_slabs(torch, qgamd, ThreadRing, m, G, steps, torch.float64, solver=1)
+    worst = _compare_slabs(torch, glob, slabs, 1e-10)
+    certs = [None] * G  # (collective in general: every slab asks in its own thread)
+    ThreadRing.run_all([lambda r=r: certs.__setitem__(r, slabs[r].pcg_certificate()) for r in range(G)])
+    with capsys.disabled():
+        print(f"\nconfig 4 PCG slabs vs one GPU (direct), {steps} steps: {worst}; certificates {certs[0]}")
+    for c in certs:
+        assert c["solves"] == steps and c["failures"] == 0 and c["worst_relres"] < 1e-12, c
 
 
 def test_config4_global_grid_against_c_oracle(env, capsys):
