@@ -168,6 +168,31 @@ def test_weak_scaling_global_grids_against_c_oracle(env, G, capsys):
         assert e < 1e-10, (n, e)
 
 
+def test_f64_8192_against_c_oracle(env, capsys):
+    """8192^2 F64 (config 5's grid at the reference's own precision, the widest square grid of
+    the size sweep) against the C oracle: 3 steps, psi and zeta < 1e-10 (north star; measured
+    7.2e-12 / 2.7e-16, r06).  Another chunk size -- another summation order of the same exact
+    solve -- moves psi by 2.3e-11: the pin's compatibility residue (sum b ~ -7.9e-16) changes in
+    its last bits and the point source it becomes is amplified by the gravest modes."""
+    torch, qgamd, _ = env
+    from oracle import qg_oracle as O
+    from oracle import qg_ref as R
+
+    N, steps = 8192, 3
+    st = qgamd.run_model_no_output(qgamd.bench_model(N, dt=60.0), nsteps=steps)
+    st.synchronize()
+    got = {n: np.stack([st.current(n, l).cpu().numpy().T for l in (1, 2)], axis=-1) for n in ("psi", "zeta")}
+    del st
+    torch.cuda.empty_cache()
+    ref = O.State(R.bench_model(N, dt=60.0)).run(steps)
+    for n in ("psi", "zeta"):
+        want = getattr(ref, n)[:, :, :, 0]
+        e = np.linalg.norm(got[n] - want) / np.linalg.norm(want)
+        with capsys.disabled():
+            print(f"\n8192^2 F64 vs C oracle, {steps} steps, {n}: {e:.3e}")
+        assert e < 1e-10, (n, e)
+
+
 @pytest.mark.parametrize("P", [8192, 16384, 32768])
 def test_device_solve_against_longdouble_on_long_grids(env, P, capsys):
     """The device's direct solve of evolve_psi!'s two systems on the weak-scaling grids
