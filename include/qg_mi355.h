@@ -322,7 +322,10 @@ int qg_comm_exchange_plan(int rank, int nranks, int send_peer[2], int send_buf[2
  * pinned[s] != 0 selects the pinned Poisson system of get_poisson_cholesky (alpha must be 0;
  * solution is 0 at interior (1,1)), then writes
  *   out_l = proj_out[2l]*x_1 + proj_out[2l+1]*x_2       with the periodic ghost ring.
- * f_2 / out_2 may be NULL when proj_in / proj_out do not need them.                        */
+ * f_2 / out_2 may be NULL when proj_in / proj_out do not need them.  M or P = 2 (spectral,
+ * one rank): the matrices exactly as construct_spA builds them, whose two-point operator is
+ * laplacian_1d_periodic(2) = [-2 1; 1 -2] (laplacian.jl:40-45), not the periodic stencil;
+ * the PCG kind refuses such domains (QG_ERR_UNSUPPORTED).                                   */
 int qg_solver_create(int64_t M, int64_t P, double dx, const double alpha[2], const int pinned[2],
                      const double proj_in[4], const double proj_out[4], int kind, int precond,
                      int device, void *stream, qg_solver **out);
