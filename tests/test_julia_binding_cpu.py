@@ -164,3 +164,76 @@ def test_dropin_slot_modes_match_the_header():
     sys.path.insert(0, os.path.join(ROOT, "julia-ocean-modelling_amd"))
     from qgamd import _lib
     assert (_lib.QG_KEEP_ORDER_SLOT1, _lib.QG_KEEP_ORDER_SLOT1_DEFERRED) == (2, 3)
+
+
+_JL_OPEN = {"module", "baremodule", "function", "struct", "if", "for", "while", "let", "begin", "do", "try",
+            "macro", "quote"}
+
+
+def _jl_strip(src):
+    """Julia source without comments, strings and character literals (for the block check)."""
+    out, i, n = [], 0, len(src)
+    while i < n:
+        if src.startswith('"""', i):
+            i = src.index('"""', i + 3) + 3
+            out.append(" ")
+            continue
+        c = src[i]
+        if c == '"':
+            j = i + 1
+            while src[j] != '"':
+                j += 2 if src[j] == "\\" else 1
+            out.append(" ")
+            i = j + 1
+            continue
+        m = re.match(r"'(\\.|[^\\'])'", src[i:i + 4]) if c == "'" else None
+        if m:
+            out.append(" ")
+            i += m.end()
+            continue
+        if src.startswith("#=", i):
+            i = src.index("=#", i) + 2
+            continue
+        if c == "#":
+            j = src.find("\n", i)
+            i = n if j < 0 else j
+            continue
+        out.append(c)
+        i += 1
+    return "".join(out)
+
+
+def jl_block_balance(src):
+    """None if every block keyword of the Julia source has its `end` (keywords and `end`
+    inside brackets -- comprehensions, `x[end]` -- do not count), else the first problem."""
+    s = _jl_strip(src)
+    stack, brack = [], 0
+    for m in re.finditer(r"[A-Za-z_][A-Za-z_0-9!]*|[\[\]\(\)\{\}]|:\w+", s):
+        t = m.group(0)
+        if t in "([{":
+            brack += 1
+        elif t in ")]}":
+            brack -= 1
+        elif brack == 0 and not t.startswith(":"):
+            if t in _JL_OPEN:
+                stack.append((t, s.count("\n", 0, m.start()) + 1))
+            elif t == "end":
+                if not stack:
+                    return f"unmatched end at line {s.count(chr(10), 0, m.start()) + 1}"
+                stack.pop()
+    if stack:
+        return f"unclosed {stack[-1][0]} from line {stack[-1][1]}"
+    return f"bracket imbalance {brack}" if brack else None
+
+
+def test_julia_blocks_are_balanced():
+    """No Julia parser here: a block-structure check of QGMI355.jl (every function / struct /
+    if / for / let / begin / do / try / module has its `end`, brackets balance), validated on a
+    copy with one `end` removed."""
+    src = open(JL).read()
+    assert jl_block_balance(src) is None
+    lines = src.split("\n")
+    ends = [i for i, l in enumerate(lines) if l.strip() == "end"]
+    assert len(ends) > 10
+    broken = "\n".join(lines[:ends[5]] + lines[ends[5] + 1:])
+    assert jl_block_balance(broken) is not None
