@@ -108,9 +108,11 @@ def compare(qgamd, torch, m, z_a, p_a, z_b, p_b, mc=8, seed=5):
     return out
 
 
-def decompose(qgamd, torch, m, steps, mc=8, seed=5):
+def decompose(qgamd, torch, m, steps, mc=8, seed=5, chunk_rows=0):
     """The F32 run of model m against the F64 run after `steps` steps (compare above), plus the
-    compatibility residue delta = -sum(b) each run's pin injected (qg_get_stats)."""
+    compatibility residue delta = -sum(b) each run's pin injected (qg_get_stats).  chunk_rows:
+    the F32 run's solver chunk (0 = automatic) -- another chunk is another summation order of
+    the scans, the singular kx = 0 line's included: another realisation of the F32 roundoff."""
     a = qgamd.run_model_no_output(m, nsteps=steps)
     a.synchronize()
     d64 = a.stats()["delta"]
@@ -118,7 +120,7 @@ def decompose(qgamd, torch, m, steps, mc=8, seed=5):
     p64 = [a.current("psi", l).clone() for l in (1, 2)]
     del a
     torch.cuda.empty_cache()
-    b = qgamd.run_model_no_output(m, nsteps=steps, dtype=torch.float32)
+    b = qgamd.run_model_no_output(m, nsteps=steps, dtype=torch.float32, chunk_rows=chunk_rows)
     b.synchronize()
     d32 = b.stats()["delta"]
     z32 = [b.current("zeta", l).clone() for l in (1, 2)]
