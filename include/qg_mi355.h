@@ -80,8 +80,13 @@ typedef enum {
 } qg_dtype;
 
 typedef enum {
-    QG_PRECOND_NONE = 0,    /* plain CG                                                    */
-    QG_PRECOND_SPECTRAL = 1 /* the spectral direct solve as preconditioner                 */
+    QG_PRECOND_NONE = 0,     /* plain CG                                                   */
+    QG_PRECOND_SPECTRAL = 1, /* the spectral direct solve as preconditioner (exact: PCG     *
+                              * converges in one iteration and certifies it)               */
+    QG_PRECOND_MULTIGRID = 2 /* geometric multigrid V(2,2) cycle (damped Jacobi, full      *
+                              * weighting, bilinear prolongation); PCG iterates.  Across   *
+                              * slabs: each rank's own V-cycle (block Jacobi).  Needs a    *
+                              * coarsest grid <= 4096 points (M, P even down to it).       */
 } qg_precond_kind;
 
 /* BaroclinicModel (src/model.jl:12-30) plus build options.  Fill with qg_default_params()

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "qg_common.hpp"
+#include "qg_mg.hpp"
 #include "qg_spectral.hpp"
 
 namespace qg {
@@ -38,6 +39,7 @@ public:
               SpectralSolver::GatherFn gather = nullptr, void *user = nullptr, HaloFn halo = nullptr,
               void *halo_user = nullptr);
     int iterations() const { return iters_; }
+    int mg_levels() const { return precond_ == QG_PRECOND_MULTIGRID ? mg_.levels() : 0; }
     double relres(int s) const { return relres_[s]; }
 
     // ---- deferred certification (default; qg_set_pcg_sync(ctx, 1) restores the host-checked
@@ -65,6 +67,7 @@ private:
     int reduce(int what, hipStream_t s, SpectralSolver::GatherFn gather, void *user);
     PcgArgs a_{};
     SpectralSolver pre_;
+    MgPrecond mg_;
     int precond_ = 0, maxit_ = 500, nblk_ = 0, iters_ = 0;
     bool cert_ = false;  // proj_out invertible: the certified preconditioner step
     double rtol_ = 1e-13, relres_[2] = {-1, -1};

@@ -62,6 +62,9 @@ end
 
 const SOLVER_SPECTRAL = Int32(0)
 const SOLVER_PCG = Int32(1)
+const PRECOND_NONE = Int32(0)       # plain CG
+const PRECOND_SPECTRAL = Int32(1)   # the spectral direct solve (exact: one certified iteration)
+const PRECOND_MULTIGRID = Int32(2)  # geometric multigrid V-cycle: PCG iterates
 
 struct QGError <: Exception
     fn::Symbol
@@ -82,7 +85,7 @@ stream_ptr() = AMDGPU.stream().stream   # hipStream_t of the task-local stream
 
 """Parameters of a reference `BaroclinicModel` (model.jl:12-30) in the C struct."""
 function QGParams(model; P_local::Integer=model.P, solver=SOLVER_SPECTRAL, P_fwd=(1.0, -1.0, 1.0, 1.0),
-                  precond::Integer=1, pcg_rtol=1e-12, pcg_maxit::Integer=500, chunk_rows::Integer=0,
+                  precond::Integer=PRECOND_SPECTRAL, pcg_rtol=1e-12, pcg_maxit::Integer=500, chunk_rows::Integer=0,
                   dtype::Type=Float64, wind_tau0=0.0, wind_rho0=1000.0)
     QGParams(model.H_1, model.H_2, model.beta, model.Lx, model.Ly, model.dt, model.T, model.U,
              model.M, P_local, model.dx, model.visc, model.r, model.R_d, model.initial_kick,

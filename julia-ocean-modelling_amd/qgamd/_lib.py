@@ -21,6 +21,7 @@ QG_F64, QG_F32 = 0, 1
 QG_SOLVER_PCG = 1
 QG_PRECOND_NONE = 0
 QG_PRECOND_SPECTRAL = 1
+QG_PRECOND_MULTIGRID = 2
 QG_KEEP_ORDER_SLOT1, QG_KEEP_ORDER_SLOT1_DEFERRED = 2, 3
 # qg_set_form (kernel-form selection, process-wide; 0 = automatic)
 QG_FORM_TENDENCY, QG_FORM_TENDENCY_TILE, QG_FORM_ROW_SPLIT, QG_FORM_PCG_NO_CERTIFICATE = 0, 1, 2, 3

@@ -1,0 +1,135 @@
+"""Matrix-free PCG with the geometric multigrid preconditioner (QG_PRECOND_MULTIGRID,
+csrc/qg_mg.hip): a Krylov solve that iterates at BASELINE sizes (VERDICT r05 missing 2; SURVEY
+7 step 5).  Against the sparse direct solve of the reference's matrices (construct_spA +
+get_*_cholesky, laplacian.jl:54-75, as oracle/qg_ref.py builds them), the C oracle's model
+run (model.jl:184-192 in the reference's loop), and, at 4096^2 (BASELINE configs 3/4), the
+device's spectral direct solve.  Tolerance: the north-star 1e-10 on psi and zeta, with the
+PCG residual target 1e-13 ("requires PCG tol <= 1e-13").  The iteration counts are
+printed and bounded: a V-cycle preconditioner keeps them nearly independent of the grid."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MG = 2  # QG_PRECOND_MULTIGRID
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import qgamd
+    from oracle import qg_oracle, qg_ref
+    from qgamd.hostcomm import ThreadRing
+
+    qg_oracle.build()
+    assert qgamd._lib.QG_PRECOND_MULTIGRID == MG
+    return torch, qgamd, qg_ref, qg_oracle, ThreadRing
+
+
+def _dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.float64).T)).cuda()
+
+
+def _rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.mark.parametrize("M,P", [(64, 64), (128, 96), (48, 40), (96, 24), (40, 24), (256, 256)])
+def test_mg_solves_match_direct(env, M, P):
+    """Both systems of evolve_psi! (pinned Poisson, modified Helmholtz) against the sparse
+    direct solve, including semi-coarsened grids (96 x 24, 40 x 24) and non-square ones."""
+    torch, qg, R, O, _ = env
+    dx = 4e6 / M
+    f = R.update_doubly_periodic_bc(R.seeded_rand(M, P, 9) - 0.5) * 1e-9
+    got_p = qg.sp_solve_poisson(M, P, dx, _dev(torch, f), kind=1, precond=MG).cpu().numpy().T
+    got_h = qg.sp_solve_modified_helmholtz(M, P, dx, _dev(torch, f), -6.25e-10, kind=1, precond=MG).cpu().numpy().T
+    ep = _rel(got_p, R.sp_solve_poisson(M, P, dx, f))
+    eh = _rel(got_h, R.sp_solve_modified_helmholtz(M, P, dx, f, -6.25e-10))
+    print(f"MG-PCG {M}x{P}: Poisson {ep:.2e}, Helmholtz {eh:.2e}")
+    assert ep < 1e-10 and eh < 1e-10, (ep, eh)
+
+
+@pytest.mark.parametrize("N,steps", [(256, 6), (1024, 4)])
+def test_mg_model_run_matches_oracle(env, N, steps):
+    """The model with QG_SOLVER_PCG + multigrid against the C oracle (exact solves): psi and
+    zeta < 1e-10 after `steps` steps; every solve iterates (> 1) and converges in few."""
+    torch, qg, R, O, _ = env
+    st = qg.initialise_model(qg.bench_model(N), solver=1, precond=MG, pcg_rtol=1e-13, pcg_maxit=200)
+    its = []
+    for t in range(1, steps + 1):
+        st.step(t)
+        s = st.stats()
+        its.append(s["iters"][0])
+        assert max(s["relres"]) <= 1e-12, s
+    ref = O.State(R.bench_model(N)).run(steps)
+    e = {n: _rel(st.to_numpy(n), getattr(ref, n)) for n in ("psi", "zeta")}
+    print(f"MG-PCG {N}^2 x {steps} steps: iterations {its}, vs C oracle {e}")
+    assert all(1 < k <= 40 for k in its), its
+    assert e["psi"] < 1e-10 and e["zeta"] < 1e-10, e
+
+
+def test_mg_at_baseline_size(env):
+    """4096^2 F64 (BASELINE configs 3/4 per GPU): MG-PCG iterates at the benchmark size and
+    matches the spectral direct solve of the same run to 1e-10 after 3 steps."""
+    torch, qg, R, O, _ = env
+    m = qg.bench_model(4096)
+    a = qg.initialise_model(m, solver=1, precond=MG, pcg_rtol=1e-13, pcg_maxit=200)
+    its = []
+    for t in range(1, 4):
+        a.step(t)
+        s = a.stats()
+        its.append(s["iters"][0])
+        assert max(s["relres"]) <= 1e-12, s
+    b = qg.run_model_no_output(m, nsteps=3)
+    torch.cuda.synchronize()
+    e = {}
+    for n in ("psi", "zeta"):
+        x, y = a.current(n, 1).double(), b.current(n, 1).double()
+        e[n] = float(torch.linalg.vector_norm(x - y) / torch.linalg.vector_norm(y))
+    print(f"MG-PCG 4096^2: iterations {its}, vs the spectral solve {e}")
+    assert all(1 < k <= 40 for k in its), its
+    assert e["psi"] < 1e-10 and e["zeta"] < 1e-10, e
+
+
+@pytest.mark.parametrize("G,N", [(2, 256), (4, 256)])
+def test_mg_slabs_match_single_gpu(env, G, N):
+    """G y-slabs over the in-process transport: PCG's operator, dots and p halos cross the
+    slabs; each rank's V-cycle is its own slab's (block Jacobi).  Same answer as one GPU."""
+    torch, qg, R, O, ThreadRing = env
+    m = qg.bench_model(N)
+    steps = 4
+    one = qg.initialise_model(m, solver=1, precond=MG, pcg_rtol=1e-13, pcg_maxit=300)
+    one.run(1, steps)
+    torch.cuda.synchronize()
+    ring = ThreadRing(G)
+    Pl = N // G
+    ranks = []
+    for r in range(G):
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            st = qg.State(m, P_local=Pl, solver=1, precond=MG, pcg_rtol=1e-13, pcg_maxit=300)
+        ring.attach(st, r)
+        ranks.append((st, s))
+
+    def work(r):
+        st, s = ranks[r]
+        with torch.cuda.stream(s):
+            st.initialise()
+            st.run(1, steps)
+            st.synchronize()
+
+    ThreadRing.run_all([lambda r=r: work(r) for r in range(G)])
+    torch.cuda.synchronize()
+    its = [st.stats()["iters"][0] for st, _ in ranks]
+    e = 0.0
+    for layer in (1, 2):
+        want = one.current("psi", layer)[1:N + 1].double()
+        got = torch.cat([st.current("psi", layer)[1:Pl + 1] for st, _ in ranks]).double()
+        e = max(e, float(torch.linalg.vector_norm(got - want) / torch.linalg.vector_norm(want)))
+    print(f"MG-PCG {G} slabs of {N}x{Pl}: iterations (last step) {its} (one GPU {one.stats()['iters'][0]}), "
+          f"psi vs one GPU {e:.2e}")
+    assert len(set(its)) == 1 and 1 < its[0] <= 120, its
+    assert e < 1e-10, e
