@@ -277,6 +277,39 @@ __global__ __launch_bounds__(PCG_T) void pcg_backproj(PcgArgs a) {
     }
 }
 
+// ---- multigrid preconditioner around the pin -------------------------------------------
+// The V-cycle approximates the inverse of the PERIODIC operator, which is singular on
+// constants for the Poisson system.  The pinned inverse is exactly T^T G T, with G the periodic
+// inverse on mean-free data, T r = r - (sum r) e_pin (the compatibility residue moved to the
+// pin, model.jl:185) and T^T z = z - z_pin (the solution shifted to vanish at the pin) -- the
+// form the spectral solve uses.  So for s = 0 the preconditioner is T^T V T: symmetric, and V
+// only ever sees mean-free right-hand sides (a constant's roundoff would otherwise be
+// amplified by the coarse grid's near-null mode and stall PCG at ~1e-13).
+// partial sums of the Poisson residual (v[1] unused)
+__global__ __launch_bounds__(PCG_T) void pcg_mg_sum(PcgArgs a) {
+    double v[2] = {0, 0};
+    PCG_FOR_POINTS(a) v[0] += a.r[0][fidx(i + 1, j + 1, a.ld)];
+    block_sumN<2>(v, a.partial);
+}
+
+// the pin's residual: -sum(r) while the V-cycle runs (T r), exactly 0 again after it
+__global__ void pcg_mg_pin_rhs(PcgArgs a, int on) {
+    if (threadIdx.x == 0 && a.pinned0 && a.rank == 0) a.r[0][fidx(1, 1, a.ld)] = on ? -a.scal[PCG_SUMR] : 0.0;
+}
+
+// this rank's part of z_pin (rank 0 holds it) for the all-gather of the rank sums
+__global__ void pcg_mg_zpin(PcgArgs a) {
+    if (threadIdx.x != 0) return;
+    a.scal[PCG_RSUM] = a.rank == 0 ? a.z[0][fidx(1, 1, a.ld)] : 0.0;
+    a.scal[PCG_RSUM + 1] = 0.0;
+}
+
+// T^T z: z - z_pin
+__global__ __launch_bounds__(PCG_T) void pcg_mg_unpin(PcgArgs a) {
+    const double zp = a.scal[PCG_ZPIN];
+    PCG_FOR_POINTS(a) a.z[0][fidx(i + 1, j + 1, a.ld)] -= zp;
+}
+
 // sum the per-block partials (fixed order) -> rank sums in scal[RSUM + 0/1]
 __global__ __launch_bounds__(1024) void pcg_rank_sum(PcgArgs a, int nblk) {
     __shared__ double s0[1024], s1[1024];
@@ -356,9 +389,16 @@ __global__ void pcg_fast_scalar(PcgArgs a, int what, const double *gathered, int
 }
 
 // combine the (gathered) rank sums and derive the next scalar
-//   what: 0 = ||b||^2, 1 = alpha = rz / pq, 2 = ||r||^2, 3 = beta = rz_new / rz (rz <- rz_new)
+//   what: 0 = ||b||^2, 1 = alpha = rz / pq, 2 = ||r||^2, 3 = beta = rz_new / rz (rz <- rz_new),
+//         4 = initial rz, 5 = sum of the Poisson residual, 6 = z at the pin
 __global__ void pcg_scalar(PcgArgs a, int what, const double *gathered, int nranks) {
     if (threadIdx.x != 0) return;
+    if (what == 5 || what == 6) {  // multigrid: sum(r_Poisson), z_pin (system 0 only)
+        double v = 0;
+        for (int g = 0; g < nranks; ++g) v += gathered[2 * g];
+        a.scal[what == 5 ? PCG_SUMR : PCG_ZPIN] = v;
+        return;
+    }
     for (int s = 0; s < 2; ++s) {
         double v = 0;
         for (int g = 0; g < nranks; ++g) v += gathered[2 * g + s];
@@ -507,8 +547,10 @@ PcgSolver::~PcgSolver() {
 }
 
 int PcgSolver::reduce(int what, hipStream_t s, SpectralSolver::GatherFn gather, void *user) {
-    pcg_rank_sum<<<1, 1024, 0, s>>>(a_, nblk_);
-    QG_LAUNCH_CHECK();
+    if (what != 6) {  // (6: the rank value is in scal[RSUM] already)
+        pcg_rank_sum<<<1, 1024, 0, s>>>(a_, nblk_);
+        QG_LAUNCH_CHECK();
+    }
     if (gather) {
         QG_CHECK(gather(user, a_.scal + PCG_RSUM, gathered_, 2, s));
         pcg_scalar<<<1, 64, 0, s>>>(a_, what, gathered_, a_.nranks);
@@ -516,6 +558,31 @@ int PcgSolver::reduce(int what, hipStream_t s, SpectralSolver::GatherFn gather, 
         pcg_scalar<<<1, 64, 0, s>>>(a_, what, a_.scal + PCG_RSUM, 1);
     }
     QG_LAUNCH_CHECK();
+    return QG_OK;
+}
+
+// z = T^T V T r (see pcg_mg_sum); the Helmholtz system (and an unpinned Poisson one) is V r
+int PcgSolver::mg_precond(hipStream_t s, SpectralSolver::GatherFn gather, void *user, HaloFn halo, void *halo_user) {
+    PcgArgs &a = a_;
+    const dim3 grid((unsigned)((a.M + PCG_T - 1) / PCG_T), (unsigned)std::min<int64_t>(a.P, PCG_ROWB));
+    const bool pin = a.pinned0 != 0;
+    if (pin) {
+        pcg_mg_sum<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce(5, s, gather, user));
+        pcg_mg_pin_rhs<<<1, 64, 0, s>>>(a, 1);
+        QG_LAUNCH_CHECK();
+    }
+    QG_CHECK(mg_.apply(a.r[0], a.r[1], a.z[0], a.z[1], s, gather, user, halo, halo_user));
+    if (pin) {
+        pcg_mg_pin_rhs<<<1, 64, 0, s>>>(a, 0);
+        QG_LAUNCH_CHECK();
+        pcg_mg_zpin<<<1, 64, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce(6, s, gather, user));
+        pcg_mg_unpin<<<grid, PCG_T, 0, s>>>(a);
+        QG_LAUNCH_CHECK();
+    }
     return QG_OK;
 }
 
@@ -586,7 +653,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         if (precond_ == QG_PRECOND_SPECTRAL) {
             QG_CHECK(pre_.solve(a.r[0], a.r[1], a.z[0], a.z[1], ghost_rows, s, gather, user));
         } else if (precond_ == QG_PRECOND_MULTIGRID) {
-            QG_CHECK(mg_.apply(a.r[0], a.r[1], a.z[0], a.z[1], s, gather, user, halo, halo_user));
+            QG_CHECK(mg_precond(s, gather, user, halo, halo_user));
         } else {
             const size_t F = (size_t)(a.M + 2) * (size_t)(a.P + 2);
             for (int k = 0; k < 2; ++k)

@@ -8,7 +8,11 @@
 namespace qg {
 
 // device scalar slots (per system s: +s)
-enum { PCG_BB = 0, PCG_RZ = 2, PCG_ALPHA = 4, PCG_BETA = 6, PCG_RR = 8, PCG_RSUM = 10, PCG_RSUM6 = 12, PCG_NSCAL = 18 };
+enum {
+    PCG_BB = 0, PCG_RZ = 2, PCG_ALPHA = 4, PCG_BETA = 6, PCG_RR = 8, PCG_RSUM = 10, PCG_RSUM6 = 12,
+    PCG_SUMR = 18, PCG_ZPIN = 19,  // multigrid: sum of the Poisson residual, the pinned value of z
+    PCG_NSCAL = 20
+};
 
 struct PcgArgs {
     int64_t M, P, ld, P_total, j_offset;
@@ -65,6 +69,7 @@ public:
 
 private:
     int reduce(int what, hipStream_t s, SpectralSolver::GatherFn gather, void *user);
+    int mg_precond(hipStream_t s, SpectralSolver::GatherFn gather, void *user, HaloFn halo, void *halo_user);
     PcgArgs a_{};
     SpectralSolver pre_;
     MgPrecond mg_;

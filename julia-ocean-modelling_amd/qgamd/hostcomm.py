@@ -24,6 +24,8 @@ def hip():
         _hip.hipMemcpy.restype = C.c_int
         _hip.hipStreamSynchronize.argtypes = [C.c_void_p]
         _hip.hipStreamSynchronize.restype = C.c_int
+        _hip.hipMemcpyAsync.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int, C.c_void_p]
+        _hip.hipMemcpyAsync.restype = C.c_int
     return _hip
 
 
@@ -36,9 +38,13 @@ def _d2h(ptr, count):
     return a
 
 
-def _h2d(ptr, a):
+def _h2d(ptr, a, stream=None):
+    """Host -> device on the rank's stream, complete on return (a null-stream copy is not
+    ordered with the library's non-blocking streams)."""
     a = np.ascontiguousarray(a, dtype=np.float64)
-    assert hip().hipMemcpy(ptr, a.ctypes.data, a.nbytes, H2D) == 0
+    h = hip()
+    assert h.hipMemcpyAsync(ptr, a.ctypes.data, a.nbytes, H2D, stream) == 0
+    assert h.hipStreamSynchronize(stream) == 0
 
 
 class TorchDistTransport:
@@ -60,7 +66,7 @@ class TorchDistTransport:
             mine = torch.from_numpy(_d2h(send, count))
             parts = [torch.empty_like(mine) for _ in range(self.dist.get_world_size(self.group))]
             self.dist.all_gather(parts, mine, group=self.group)
-            _h2d(recv, torch.cat(parts).numpy())
+            _h2d(recv, torch.cat(parts).numpy(), stream)
             return 0
         except Exception as e:  # never let an exception cross the C boundary
             print("allgather callback failed:", e, flush=True)
@@ -90,7 +96,7 @@ class TorchDistTransport:
             for r in reqs:
                 r.wait()
             for k in range(nr):
-                _h2d(rp[k], bufs[k].numpy())
+                _h2d(rp[k], bufs[k].numpy(), stream)
             return 0
         except Exception as e:
             print("sendrecv callback failed:", e, flush=True)
@@ -139,8 +145,11 @@ class ThreadRing:
         from ._lib import call
 
         h = hip()
-        h.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
         D2D = 3
+        # The copies run on the rank's own stream and complete before the second barrier: a
+        # device-to-device hipMemcpy may return before its copy has run, and on the null stream
+        # it is not ordered with the ranks' (non-blocking) streams -- a receiver's next kernel
+        # could read, or a sender's next pack kernel overwrite, a buffer still being copied.
 
         def ag(user, send, recv, count, stream):
             try:
@@ -149,8 +158,10 @@ class ThreadRing:
                 self.gather[rank] = (int(send), int(count))
                 self._wait()
                 for q, (ptr, n) in enumerate(self.gather):
-                    if n != count or h.hipMemcpy(int(recv) + 8 * q * count, ptr, 8 * count, D2D) != 0:
+                    if n != count or h.hipMemcpyAsync(int(recv) + 8 * q * count, ptr, 8 * count, D2D, stream) != 0:
                         return 1
+                if h.hipStreamSynchronize(stream) != 0:
+                    return 1
                 self._wait()
                 return 0
             except Exception as e:  # includes threading.BrokenBarrierError
@@ -171,8 +182,10 @@ class ThreadRing:
                     taken[peer] = n + 1
                     mine = [m for m in self.sends[peer] if m[0] == rank]
                     _, ptr, cnt = mine[n]
-                    if cnt != rc[k] or h.hipMemcpy(int(rp[k]), ptr, 8 * cnt, D2D) != 0:
+                    if cnt != rc[k] or h.hipMemcpyAsync(int(rp[k]), ptr, 8 * cnt, D2D, stream) != 0:
                         return 1
+                if h.hipStreamSynchronize(stream) != 0:
+                    return 1
                 self._wait()
                 return 0
             except Exception as e:
