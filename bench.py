@@ -399,7 +399,7 @@ def mg_variant(qgamd, m, n, K, torch):
     return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K,
             "iters_per_step": its, "relres_poisson_helmholtz": s["relres"],
             "note": "same workload, evolve_psi! by PCG with a geometric multigrid V(2,2) preconditioner "
-                    "(damped Jacobi, full weighting, bilinear prolongation): iterates ~14 times per solve "
+                    "(damped Jacobi, full weighting, bilinear prolongation): iterates ~10 times per solve "
                     "at every size; the spectral direct solve (the headline) is its exact-inverse limit"}
 
 
