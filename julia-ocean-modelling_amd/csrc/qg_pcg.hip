@@ -244,10 +244,13 @@ __global__ __launch_bounds__(PCG_T) void pcg_update(PcgArgs a) {
 // the pin's own identity row, whose residual it ignores (its compatibility shift absorbs it);
 // completing the inverse there (z = r on that row) lets PCG remove the pin-row residual that
 // roundoff in the pin subtraction leaves in x.
-__global__ __launch_bounds__(PCG_T) void pcg_dot_rz(PcgArgs a) {
+// unpin (multigrid): z_0 -= z_pin first (T^T z, see pcg_mg_sum), in the same pass
+__global__ __launch_bounds__(PCG_T) void pcg_dot_rz(PcgArgs a, int unpin) {
     double v[2] = {0, 0};
+    const double zp = unpin ? a.scal[PCG_ZPIN] : 0.0;
     PCG_FOR_POINTS(a) {
         const size_t o = fidx(i + 1, j + 1, a.ld);
+        if (unpin) a.z[0][o] -= zp;
         if (is_pin(a, i, j)) a.z[0][o] = a.r[0][o];
         v[0] += a.r[0][o] * a.z[0][o];
         v[1] += a.r[1][o] * a.z[1][o];
@@ -302,12 +305,6 @@ __global__ void pcg_mg_zpin(PcgArgs a) {
     if (threadIdx.x != 0) return;
     a.scal[PCG_RSUM] = a.rank == 0 ? a.z[0][fidx(1, 1, a.ld)] : 0.0;
     a.scal[PCG_RSUM + 1] = 0.0;
-}
-
-// T^T z: z - z_pin
-__global__ __launch_bounds__(PCG_T) void pcg_mg_unpin(PcgArgs a) {
-    const double zp = a.scal[PCG_ZPIN];
-    PCG_FOR_POINTS(a) a.z[0][fidx(i + 1, j + 1, a.ld)] -= zp;
 }
 
 // sum the per-block partials (fixed order) -> rank sums in scal[RSUM + 0/1]
@@ -579,9 +576,7 @@ int PcgSolver::mg_precond(hipStream_t s, SpectralSolver::GatherFn gather, void *
         QG_LAUNCH_CHECK();
         pcg_mg_zpin<<<1, 64, 0, s>>>(a);
         QG_LAUNCH_CHECK();
-        QG_CHECK(reduce(6, s, gather, user));
-        pcg_mg_unpin<<<grid, PCG_T, 0, s>>>(a);
-        QG_LAUNCH_CHECK();
+        QG_CHECK(reduce(6, s, gather, user));  // (z -= z_pin: in the pcg_dot_rz that follows)
     }
     return QG_OK;
 }
@@ -668,6 +663,8 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         }
         return QG_OK;
     };
+    // the multigrid form's T^T step rides on the pcg_dot_rz after each preconditioner call
+    const int unpin = precond_ == QG_PRECOND_MULTIGRID && a.pinned0 ? 1 : 0;
     double host[PCG_NSCAL];
     iters_ = 0;
     relres_[0] = relres_[1] = -1;
@@ -713,7 +710,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         pcg_cert_restart<<<grid, PCG_T, 0, s>>>(a);  // x0 = z0, r0 = b - B z0; bb already set
         QG_LAUNCH_CHECK();
         QG_CHECK(precond());
-        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
+        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a, unpin);
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce(4, s, gather, user));
         pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 1);
@@ -754,7 +751,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce(0, s, gather, user));
         QG_CHECK(precond());
-        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
+        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a, unpin);
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce(4, s, gather, user));
         pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 1);
@@ -777,7 +774,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
         if (resume) {  // z1 = M^-1 r1, beta, p1 = z1 + beta p0 (the tail of iteration 1)
             resume = false;
             QG_CHECK(precond());
-            pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
+            pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a, unpin);
             QG_LAUNCH_CHECK();
             QG_CHECK(reduce(3, s, gather, user));
             pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 0);
@@ -812,7 +809,7 @@ int PcgSolver::solve(const double *in1, const double *in2, double *out1, double 
             break;
         }
         QG_CHECK(precond());
-        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a);
+        pcg_dot_rz<<<grid, PCG_T, 0, s>>>(a, unpin);
         QG_LAUNCH_CHECK();
         QG_CHECK(reduce(3, s, gather, user));
         pcg_pupdate<<<grid, PCG_T, 0, s>>>(a, 0);

@@ -27,7 +27,8 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl", gather="rccl", devices=False):
+def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl", gather="rccl", devices=False,
+            kw=None):
     import sys
 
     sys.path[:0] = [ROOT, os.path.join(ROOT, "julia-ocean-modelling_amd")]
@@ -53,7 +54,7 @@ def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl"
         uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
     dist.broadcast(uid, 0)
     m = qgamd.bench_model(M, P=P)
-    st = qgamd.State(m, P_local=P // world, solver=solver)
+    st = qgamd.State(m, P_local=P // world, solver=solver, **(kw or {}))
     st.comm_init(world, rank, bytes(uid.numpy().tobytes()))
     if halo != "rccl":
         st.set_halo_transport(halo)
@@ -69,13 +70,13 @@ def _worker(rank, world, port, M, P, steps, outdir, solver, overlap, halo="rccl"
     dist.destroy_process_group()
 
 
-def _run(world, M, P, steps, d, solver, overlap, halo="rccl", gather="rccl", devices=False):
+def _run(world, M, P, steps, d, solver, overlap, halo="rccl", gather="rccl", devices=False, kw=None):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, M, P, steps, d, solver, overlap, halo, gather,
-                                               devices))
+                                               devices, kw))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -89,23 +90,30 @@ def _run(world, M, P, steps, d, solver, overlap, halo="rccl", gather="rccl", dev
     return [dict(np.load(os.path.join(d, f"rank{r}.npz"))) for r in range(world)]
 
 
-@pytest.mark.parametrize("world,M,P,steps,solver,overlap",
-                         [(2, 64, 64, 6, 0, True), (2, 64, 64, 6, 0, False), (4, 64, 64, 5, 0, True),
-                          (2, 64, 64, 5, 1, True), (2, 1024, 128, 4, 0, True)])
-def test_rccl_slabs_match_single_gpu(world, M, P, steps, solver, overlap):
+MG = {"precond": 2, "pcg_rtol": 1e-13}  # QG_PRECOND_MULTIGRID
+MG_PCG = dict(MG, solver=1)
+
+
+@pytest.mark.parametrize("world,M,P,steps,solver,overlap,kw",
+                         [(2, 64, 64, 6, 0, True, None), (2, 64, 64, 6, 0, False, None), (4, 64, 64, 5, 0, True, None),
+                          (2, 64, 64, 5, 1, True, None), (2, 1024, 128, 4, 0, True, None),
+                          (2, 128, 128, 4, 1, True, MG), (4, 256, 256, 3, 1, True, MG)])
+def test_rccl_slabs_match_single_gpu(world, M, P, steps, solver, overlap, kw):
     """solver 0 = spectral (halo send/recv + record all-gather), 1 = PCG with the spectral
-    preconditioner (its dot-product gathers and z halo also cross RCCL)."""
+    preconditioner (its dot-product gathers and z halo also cross RCCL) or, kw = MG, the
+    multigrid V-cycle (its per-level ghost-row refreshes and the agglomerated coarse grid's
+    all-gathers over RCCL too)."""
     import torch
 
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import qgamd
 
-    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps, solver=solver)
+    ref = qgamd.run_model_no_output(qgamd.bench_model(M, P=P), nsteps=steps, solver=solver, **(kw or {}))
     torch.cuda.synchronize()
     g = {n: ref.to_numpy(n) for n in ("zeta", "psi", "f_store")}
     with tempfile.TemporaryDirectory() as d:
-        loc = _run(world, M, P, steps, d, solver, overlap)
+        loc = _run(world, M, P, steps, d, solver, overlap, kw=kw)
     Pl = P // world
     for r in range(world):
         for n in ("zeta", "psi", "f_store"):
@@ -172,7 +180,7 @@ def test_peer_transports_across_devices_bit_identical(halo, gather, overlap):
 
 # ---- BASELINE configs 4 and 5 at their workload size over multi-rank RCCL ----------------
 
-def _config_worker(rank, world, port, M, steps, outdir, f32):
+def _config_worker(rank, world, port, M, steps, outdir, f32, kw=None):
     """One slab of an M x (world*M) model over RCCL; saves its current zeta and psi slots
     (both layers, ghost rows included) for the parent's comparison with one GPU."""
     import sys
@@ -199,7 +207,7 @@ def _config_worker(rank, world, port, M, steps, outdir, f32):
         uid.copy_(torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8))
     dist.broadcast(uid, 0)
     m = qgamd.bench_model(M, P=world * M, dt=60.0)
-    st = qgamd.State(m, P_local=M, dtype=torch.float32 if f32 else torch.float64)
+    st = qgamd.State(m, P_local=M, dtype=torch.float32 if f32 else torch.float64, **(kw or {}))
     st.comm_init(world, rank, bytes(uid.numpy().tobytes()))
     st.initialise()
     st.run(1, steps)
@@ -213,12 +221,15 @@ def _config_worker(rank, world, port, M, steps, outdir, f32):
 
 # bars: test_gpu_configs.py's (F32: zeta < 16 eps_32, psi by the mechanism's derived bars of
 # tests/f32_model.py -- the white-noise field's rounding amplified by the gravest Poisson modes)
-@pytest.mark.parametrize("world,M,steps,f32,tol", [(4, 4096, 4, False, {"zeta": 1e-10, "psi": 1e-10}),
-                                                   (8, 8192, 3, True, {"zeta": 16 * 2.0 ** -24, "psi": 1.0})])
-def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, capsys):
+@pytest.mark.parametrize("world,M,steps,f32,tol,kw", [(4, 4096, 4, False, {"zeta": 1e-10, "psi": 1e-10}, None),
+                                                      (8, 8192, 3, True, {"zeta": 16 * 2.0 ** -24, "psi": 1.0}, None),
+                                                      (4, 4096, 3, False, {"zeta": 1e-10, "psi": 1e-10}, MG_PCG)])
+def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, kw, capsys):
     """config 4: four 4096^2 F64 slabs (global 4096 x 16384); config 5: eight 8192^2 F32 slabs
     (global 8192 x 65536) -- over multi-rank RCCL, against the single-GPU run of the global
-    model (the same bars as the host-transport form in test_gpu_configs.py)."""
+    model (the same bars as the host-transport form in test_gpu_configs.py).  kw = MG_PCG:
+    config 4 as BASELINE words it ("RCCL halo + PCG all-reduce"), the PCG iterating with the
+    multigrid preconditioner on the slabs, against the spectral direct solve on one GPU."""
     import torch
     import torch.multiprocessing as mp
 
@@ -229,7 +240,8 @@ def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, capsys):
     with tempfile.TemporaryDirectory() as d:
         ctx = mp.get_context("spawn")
         port = _free_port()
-        procs = [ctx.Process(target=_config_worker, args=(r, world, port, M, steps, d, f32)) for r in range(world)]
+        procs = [ctx.Process(target=_config_worker, args=(r, world, port, M, steps, d, f32, kw))
+                 for r in range(world)]
         for p in procs:
             p.start()
         for p in procs:
@@ -265,7 +277,8 @@ def test_rccl_config_slabs_match_single_gpu(world, M, steps, f32, tol, capsys):
                               [glob.current("zeta", 1), glob.current("zeta", 2)],
                               [glob.current("psi", 1), glob.current("psi", 2)], mc=8)
     with capsys.disabled():
-        print(f"\nRCCL {world} x {M}^2 {'F32' if f32 else 'F64'} slabs vs one GPU, {steps} steps: {worst}"
+        print(f"\nRCCL {world} x {M}^2 {'F32' if f32 else 'F64'} slabs{' (MG-PCG)' if kw else ''} vs one GPU, "
+              f"{steps} steps: {worst}"
               + (f"; {F32.fmt(rec)}; bars {F32.bars(rec)}" if rec else ""))
     assert all(worst[n] < tol[n] for n in worst), worst
     if rec:
