@@ -20,10 +20,11 @@ for f in ["$O/bench_driver_%d.json" % k for k in (1, 2, 3)] + ["$O/bench_default
           round(d["step_roofline"]["solve_ms"] * 1e3, 1), "us; dropin", round(d["dropin"]["vs_qg_run_step"], 3),
           "slot1", round(d["dropin_slot1"]["vs_qg_run_step"], 3), "slot1_deferred",
           round(d["dropin_slot1_deferred"]["vs_qg_run_step"], 3), "; pcg", round(d["pcg_solver"]["value"], 1),
+          "; mg-pcg", round(d["mg_pcg_solver"]["value"], 1), d["mg_pcg_solver"]["iters_per_step"][-1],
           "; cpu", round(d["cpu_baseline"]["value"], 3), d["cpu_baseline"]["cores"])
 PY
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o drv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc-live --no-reference-runs --cpu-steps 0 > $R/$O/prof.log 2>&1 || exit 4
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o drv -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc-live --no-reference-runs --cpu-steps 0 --mg-steps 0 > $R/$O/prof.log 2>&1 || exit 4
 cut -d, -f1-4 $R/$O/prof/drv_kernel_stats.csv | head -8 | tee -a $R/$O/summary.txt
 cd $R && bash tools/pmc.sh ev_$TAG > $O/pmc.log 2>&1 || exit 5
 echo done | tee -a $O/summary.txt

@@ -6,7 +6,7 @@
 TAG=${1:-r06f}
 R=$GRAFT_REPO_ROOT; cd $R || exit 1
 O=gpurun_out/ev_$TAG; mkdir -p $O
-B="--cpu-steps 0 --cpu-steps-1t 0 --pcg-steps 0 --dropin-steps 0 --no-pmc-live --no-reference-runs"
+B="--cpu-steps 0 --cpu-steps-1t 0 --pcg-steps 0 --mg-steps 0 --dropin-steps 0 --no-pmc-live --no-reference-runs"
 for k in 1 2 3; do
   timeout -k 10 300 python bench.py --n 8192 --dtype f32 --steps 50 --warmup 5 $B > $O/c5_$k.json 2> $O/c5_$k.err || exit 1
 done
