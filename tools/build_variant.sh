@@ -5,7 +5,7 @@ set -e
 NAME=$1; SRC=$2; shift 2
 PKG=/root/repo/julia-ocean-modelling_amd
 OUT=/tmp/variant_$NAME; rm -rf $OUT; mkdir -p $OUT $PKG/lib/exp
-for f in qg_stencil qg_spectral qg_pcg qg_capi qg_comm qg_diag; do
+for f in qg_stencil qg_spectral qg_pcg qg_capi qg_comm qg_diag qg_mg; do
   X=""; [ $f = qg_stencil ] && X="-ffp-contract=off"
   /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -I/root/repo/include -I$SRC -Wall -Wno-unused-function $X "$@" -c $SRC/$f.hip -o $OUT/$f.o &
 done
