@@ -68,6 +68,9 @@ def parse(argv=None):
     ap.add_argument("--solver", choices=("spectral", "pcg"), default="spectral",
                     help="streamfunction inversion: direct spectral (default) or matrix-free PCG "
                          "preconditioned by the spectral solve")
+    ap.add_argument("--precond", choices=("spectral", "mg", "none"), default="spectral",
+                    help="--solver pcg: its preconditioner (the spectral solve: one certified "
+                         "iteration; mg: the multigrid V-cycle, ~10 iterations; none: plain CG)")
     ap.add_argument("--dtype", choices=("f64", "f32"), default="f64",
                     help="state precision: f64 (the reference's, default) or f32 (BASELINE config 5)")
     ap.add_argument("--pcg-steps", type=int, default=20,
@@ -692,7 +695,10 @@ def main():
     t_setup = time.perf_counter()
     solver = qgamd._lib.QG_SOLVER_PCG if args.solver == "pcg" else qgamd._lib.QG_SOLVER_SPECTRAL
     tdtype = torch.float32 if args.dtype == "f32" else torch.float64
-    st = qgamd.State(m, solver=solver, chunk_rows=args.chunk_rows, P_local=n, dtype=tdtype)
+    precond = {"spectral": qgamd._lib.QG_PRECOND_SPECTRAL, "mg": qgamd._lib.QG_PRECOND_MULTIGRID,
+               "none": qgamd._lib.QG_PRECOND_NONE}[args.precond]
+    st = qgamd.State(m, solver=solver, chunk_rows=args.chunk_rows, P_local=n, dtype=tdtype, precond=precond,
+                     **({"pcg_maxit": 20000} if args.precond == "none" else {}))
     if world == 1 and args.comm_self:
         import ctypes as C
         buf = C.create_string_buffer(128)
@@ -986,7 +992,9 @@ def main():
             "parallelism": f"y-slab x{world}" if world > 1 else ("single GPU, 1-rank RCCL ring" if args.comm_self
                                                                  else "single GPU"),
             "solver": ("spectral (x-DFT + parallel cyclic tridiagonal in y, direct)" if args.solver == "spectral"
-                       else "matrix-free PCG on the 5-point operator, spectral preconditioner"),
+                       else "matrix-free PCG on the 5-point operator, " + {
+                           "spectral": "spectral preconditioner", "mg": "multigrid V-cycle preconditioner",
+                           "none": "no preconditioner"}[args.precond]),
             "finite": finite,
             "transport": (("rccl, all ranks on one GPU: network transport over loopback (--one-gpu rehearsal, "
                            "not xGMI, not a measurement)" if one_gpu else args.transport)

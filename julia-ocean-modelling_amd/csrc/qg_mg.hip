@@ -219,8 +219,11 @@ __global__ __launch_bounds__(MG_T) void mg_coarse(MgCoarse a) {
 
 // ------------------------------------------------------------------------------------
 // Levels: slab levels (nranks > 1) halve while their rows can (even, >= 8) and the level has
-// > 64 points; then the global grid of the same resolution is gathered, and global levels
-// halve down to <= 64 points.
+// more than MG_AGG_POINTS points; then the global grid of the same resolution is gathered, and
+// global levels halve down to <= 64 points.  (Below ~4096 points per rank a level's work is a
+// few microseconds and its four ghost-row exchanges are the whole cost: those levels are
+// cycled redundantly on every rank instead.)
+constexpr int64_t MG_AGG_POINTS = 4096;
 static int plan_levels(int64_t M, int64_t P, int nranks, MgLevel *lv) {
     lv[0] = MgLevel{};
     lv[0].M = M;
@@ -232,7 +235,7 @@ static int plan_levels(int64_t M, int64_t P, int nranks, MgLevel *lv) {
         const int rx = f.M % 2 == 0 && f.M >= 8, ry = f.P % 2 == 0 && f.P >= 8;
         MgLevel c{};
         if (f.slab) {
-            if (f.M * f.P > 64 && ry) {
+            if (f.M * f.P > MG_AGG_POINTS && ry) {
                 c.M = rx ? f.M / 2 : f.M;
                 c.P = f.P / 2;
                 c.rx = rx;
