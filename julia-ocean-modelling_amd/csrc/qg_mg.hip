@@ -221,7 +221,7 @@ __global__ __launch_bounds__(MG_T) void mg_coarse(MgCoarse a) {
 // Levels: slab levels (nranks > 1) halve while their rows can (even, >= 8) and the level has
 // more than MG_AGG_POINTS points; then the global grid of the same resolution is gathered, and
 // global levels halve down to <= 64 points.  (Below ~4096 points per rank a level's work is a
-// few microseconds and its four ghost-row exchanges are the whole cost: those levels are
+// few microseconds and its five ghost-row exchanges are the whole cost: those levels are
 // cycled redundantly on every rank instead.)
 constexpr int64_t MG_AGG_POINTS = 4096;
 static int plan_levels(int64_t M, int64_t P, int nranks, MgLevel *lv) {
