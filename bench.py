@@ -399,8 +399,19 @@ def mg_variant(qgamd, m, n, K, torch):
     el = time.perf_counter() - t0
     s = st.stats()
     del st
+    # B_step = 8 N^2 (W_fix + W_it (k_P + k_H)) bytes, W_fix = 28 words/pt; W_it per
+    # system and iteration = PCG's vectors 14 (apply 2, update 6, r.z 2.5, p 3, sum(r) 0.5) +
+    # the V-cycle 14.5 per fine point (pre 2, residual 3, restriction 1.25, prolongation 2.25,
+    # two sweeps 6) x 4/3 over the levels = 33.3 words/pt
+    w_it, w_fix = 14.0 + 14.5 * 4.0 / 3.0, 28.0
+    kk = sum(its) / len(its)
+    b_step = 8.0 * m.M * m.P * (w_fix + w_it * 2 * kk)
+    ach = b_step / (el / K) / 1e9
     return {"value": K / el, "unit": "timesteps/s", "steps": K, "ms_per_step": el * 1e3 / K,
             "iters_per_step": its, "relres_poisson_helmholtz": s["relres"],
+            "roofline": {"bound": "hbm", "achieved": ach, "peak": 8000.0, "unit": "GB/s", "frac": ach / 8000.0,
+                         "words_per_point": {"W_fix": w_fix, "W_it": round(w_it, 2)},
+                         "algorithmic_bytes_per_step": b_step},
             "note": "same workload, evolve_psi! by PCG with a geometric multigrid V(2,2) preconditioner "
                     "(damped Jacobi, full weighting, bilinear prolongation): iterates ~10 times per solve "
                     "at every size; the spectral direct solve (the headline) is its exact-inverse limit"}
