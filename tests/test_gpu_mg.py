@@ -133,3 +133,14 @@ def test_mg_slabs_match_single_gpu(env, G, N):
           f"psi vs one GPU {e:.2e}")
     assert len(set(its)) == 1 and 1 < its[0] <= 120, its
     assert e < 1e-10, e
+
+
+@pytest.mark.parametrize("M,P", [(4099, 16), (4097, 4097)])
+def test_mg_refuses_grids_without_a_small_coarsest_level(env, M, P):
+    """Odd (here prime-ish) dimensions do not coarsen: when the coarsest grid would exceed
+    MG_COARSE_MAX points the context refuses the configuration (QG_ERR_UNSUPPORTED) at
+    creation instead of running a cycle that cannot converge fast."""
+    torch, qg, R, O, _ = env
+    with pytest.raises(qg.QGError) as e:
+        qg.State(qg.bench_model(M, P=P), solver=1, precond=MG)
+    assert e.value.status == -2
