@@ -144,3 +144,19 @@ def test_mg_refuses_grids_without_a_small_coarsest_level(env, M, P):
     with pytest.raises(qg.QGError) as e:
         qg.State(qg.bench_model(M, P=P), solver=1, precond=MG)
     assert e.value.status == -2
+
+
+def test_mg_long_run_tracks_the_direct_solve(env):
+    """1024^2 (BASELINE config 2's grid), 200 steps: the iterating PCG stays on the spectral
+    direct solve's trajectory (each solve to 1e-13) -- no drift from the solve's residual."""
+    torch, qg, R, O, _ = env
+    m = qg.bench_model(1024)
+    a = qg.run_model_no_output(m, nsteps=200, solver=1, precond=MG, pcg_rtol=1e-13, pcg_maxit=200)
+    b = qg.run_model_no_output(m, nsteps=200)
+    torch.cuda.synchronize()
+    e = {}
+    for n in ("psi", "zeta"):
+        x, y = a.current(n, 1).double(), b.current(n, 1).double()
+        e[n] = float(torch.linalg.vector_norm(x - y) / torch.linalg.vector_norm(y))
+    print(f"MG-PCG 1024^2 x 200 steps vs the spectral solve: {e}; last iterations {a.stats()['iters']}")
+    assert e["psi"] < 1e-10 and e["zeta"] < 1e-10, e
