@@ -160,3 +160,24 @@ def test_mg_long_run_tracks_the_direct_solve(env):
         e[n] = float(torch.linalg.vector_norm(x - y) / torch.linalg.vector_norm(y))
     print(f"MG-PCG 1024^2 x 200 steps vs the spectral solve: {e}; last iterations {a.stats()['iters']}")
     assert e["psi"] < 1e-10 and e["zeta"] < 1e-10, e
+
+
+@pytest.mark.parametrize("opt", ["P_fwd", "wind"])
+def test_mg_with_the_f3_options(env, opt):
+    """SURVEY 8(f)-3 with the iterating PCG: the physical back-projection P_matrix(H_1, H_2)
+    and the wind-forcing extension, 30 steps against the C oracle run with the same option
+    (the spectral-preconditioned form's test is test_gpu_parity.py)."""
+    torch, qg, R, O, _ = env
+    M, P = 64, 48
+    m = qg.bench_model(M, P=P)
+    if opt == "P_fwd":
+        Pf = R.P_matrix(m.H_1, m.H_2)
+        st = qg.run_model_no_output(m, nsteps=30, solver=1, precond=MG, pcg_rtol=1e-13, P_fwd=Pf)
+        ref = O.State(R.bench_model(M, P=P), P_fwd=Pf).run(30)
+    else:
+        wind = (0.1, 1000.0)
+        st = qg.run_model_no_output(m, nsteps=30, solver=1, precond=MG, pcg_rtol=1e-13, wind=wind)
+        ref = O.State(R.bench_model(M, P=P), wind=wind).run(30)
+    e = {n: _rel(st.to_numpy(n), getattr(ref, n)) for n in ("psi", "zeta")}
+    print(f"MG-PCG {M}x{P} with {opt}, 30 steps vs C oracle: {e}")
+    assert e["psi"] < 1e-10 and e["zeta"] < 1e-10, e
