@@ -33,7 +33,6 @@ public:
     // and two all-gathers of the agglomerated level).
     int apply(const double *r0, const double *r1, double *z0, double *z1, hipStream_t s, GatherFn gather = nullptr,
               void *user = nullptr, HaloFn halo = nullptr, void *halo_user = nullptr);
-    int levels() const { return nl_; }
     static bool supports(int64_t M, int64_t P, int nranks);
 
 private:

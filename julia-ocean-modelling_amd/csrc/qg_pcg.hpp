@@ -43,7 +43,6 @@ public:
               SpectralSolver::GatherFn gather = nullptr, void *user = nullptr, HaloFn halo = nullptr,
               void *halo_user = nullptr);
     int iterations() const { return iters_; }
-    int mg_levels() const { return precond_ == QG_PRECOND_MULTIGRID ? mg_.levels() : 0; }
     double relres(int s) const { return relres_[s]; }
 
     // ---- deferred certification (default; qg_set_pcg_sync(ctx, 1) restores the host-checked
