@@ -28,9 +28,10 @@ public:
     // B_s = -(5-point Laplacian + alpha_s), alpha_s <= 0.
     int init(int64_t M, int64_t P, int rank, int nranks, double dx, const double alpha[2]);
     ~MgPrecond();
-    // z_s = V(r_s), s = 0, 1: (M+2, P+2) fields; r's interior is read, z's interior written
-    // (its ghost rows are used as scratch).  nranks > 1: every rank calls it (halo refreshes
-    // and two all-gathers of the agglomerated level).
+    // z_s = V(r_s), s = 0, 1: (M+2, P+2) fields; r's interior is read, z's interior written;
+    // the ghost rows of both are scratch (a slab refreshes them from its neighbours).
+    // nranks > 1: every rank calls it (ghost-row refreshes and the agglomerated level's two
+    // all-gathers are collective).
     int apply(const double *r0, const double *r1, double *z0, double *z1, hipStream_t s, GatherFn gather = nullptr,
               void *user = nullptr, HaloFn halo = nullptr, void *halo_user = nullptr);
     static bool supports(int64_t M, int64_t P, int nranks);
