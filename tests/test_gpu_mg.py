@@ -71,11 +71,13 @@ def test_mg_model_run_matches_oracle(env, N, steps):
     assert e["psi"] < 1e-10 and e["zeta"] < 1e-10, e
 
 
-def test_mg_at_baseline_size(env):
-    """4096^2 F64 (BASELINE configs 3/4 per GPU): MG-PCG iterates at the benchmark size and
-    matches the spectral direct solve of the same run to 1e-10 after 3 steps."""
+@pytest.mark.parametrize("N", [4096, 8192])
+def test_mg_at_baseline_size(env, N):
+    """4096^2 F64 (BASELINE configs 3/4 per GPU) and 8192^2 (config 5's grid, here in F64: PCG
+    runs F64 states): MG-PCG iterates at the benchmark size and matches the spectral direct
+    solve of the same run to 1e-10 after 3 steps."""
     torch, qg, R, O, _ = env
-    m = qg.bench_model(4096)
+    m = qg.bench_model(N)
     a = qg.initialise_model(m, solver=1, precond=MG, pcg_rtol=1e-13, pcg_maxit=200)
     its = []
     for t in range(1, 4):
@@ -89,7 +91,7 @@ def test_mg_at_baseline_size(env):
     for n in ("psi", "zeta"):
         x, y = a.current(n, 1).double(), b.current(n, 1).double()
         e[n] = float(torch.linalg.vector_norm(x - y) / torch.linalg.vector_norm(y))
-    print(f"MG-PCG 4096^2: iterations {its}, vs the spectral solve {e}")
+    print(f"MG-PCG {N}^2: iterations {its}, vs the spectral solve {e}")
     assert all(1 < k <= 40 for k in its), its
     assert e["psi"] < 1e-10 and e["zeta"] < 1e-10, e
 
