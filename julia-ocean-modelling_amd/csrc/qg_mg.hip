@@ -3,21 +3,23 @@
 //
 // Operator per level and system: B_s = -(cx (E + W - 2) + cy (N + S - 2) + alpha_s), the
 // 5-point form of construct_spA (src/schemes/laplacian.jl:54-75) with hx, hy of the level,
-// periodic in x and y.  The Poisson system's pin (laplacian.jl:70-73) is left to PCG: its
-// iterates keep the pinned unknown at exactly 0 and pcg_dot_rz zeroes z there, so the
-// preconditioner it sees is E V E (E: the projection off the pin), SPD on that subspace.
+// periodic in x and y.  The Poisson system's pin (laplacian.jl:70-73) is handled around the
+// cycle by PCG (qg_pcg.hip, mg_precond): z = T^T V T r, T moving the compatibility residue
+// sum(r) to the pin, T^T shifting z to vanish there -- the pinned inverse's exact form.
 //
-// V(2,2): two damped-Jacobi sweeps from zero (one fused pass), the residual restricted by full
-// weighting (R = c P^T in every direction that coarsens, so the cycle is symmetric), the coarse
-// problem rediscretised at 2h, bilinear prolongation, two sweeps; the coarsest grid (<= MG_COARSE_MAX
-// points) gets Jacobi sweeps inside one workgroup's LDS.  A dimension coarsens while it is
-// even and >= 8 (semi-coarsening when only one does), down to <= 64 points.
+// V(2,2): two damped-Jacobi sweeps from zero (one fused pass), the residual restricted by
+// full weighting (R = c P^T in every direction that coarsens, so the cycle is symmetric), the
+// coarse problem rediscretised at 2h, bilinear prolongation, two sweeps; the coarsest grid
+// (<= MG_COARSE_MAX points) gets Jacobi sweeps inside one workgroup's LDS.  A dimension
+// coarsens while it is even and >= 8 (semi-coarsening when only one does), down to <= 64
+// points.
 //
 // Across y-slabs the cycle is the same global one: a slab level takes its y neighbours from
 // ghost rows the transport refreshes before every stencil pass that reads them (comm_halo),
-// and once a slab can no longer halve its rows the level's right-hand side is all-gathered
-// into the global grid (one contiguous block of rows per rank), which every rank then cycles
-// redundantly and identically; each rank takes its own rows of the result back.
+// and once a slab level is down to MG_AGG_POINTS points (or cannot halve its rows) its
+// right-hand side is all-gathered into the global grid (one contiguous block of rows per
+// rank), which every rank then cycles redundantly and identically; each rank takes its own
+// rows of the result back.
 //
 // Every stage is a stencil pass over rows: HBM-bound, one thread per point of a row segment,
 // rows strided over the grid's y workgroups.  Sums run in a fixed order: deterministic.
